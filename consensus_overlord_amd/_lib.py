@@ -1,0 +1,62 @@
+"""ctypes binding of libovhip.so (include/ovhip.h). No fallback: if the HIP library is
+missing or cannot be loaded, importing the product raises."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libovhip.so")
+
+_u8p = ctypes.c_char_p
+_sz = ctypes.c_size_t
+_szp = ctypes.POINTER(ctypes.c_size_t)
+_vp = ctypes.c_void_p
+
+# (name, restype, argtypes) -- mirrors include/ovhip.h
+SIGNATURES = [
+    ("ovh_create", _vp, [ctypes.c_int, _u8p, _sz, ctypes.c_uint32]),
+    ("ovh_destroy", None, [_vp]),
+    ("ovh_stream", _vp, [_vp]),
+    ("ovh_sm3", ctypes.c_int, [_u8p, _sz, _u8p]),
+    ("ovh_sign", ctypes.c_int, [_vp, _u8p, _sz, _u8p, _sz, _u8p]),
+    ("ovh_sk_to_pk", ctypes.c_int, [_vp, _u8p, _sz, _u8p]),
+    ("ovh_verify", ctypes.c_int, [_vp, _u8p, _sz, _u8p, _sz, _u8p, _sz]),
+    ("ovh_aggregate_sigs", ctypes.c_int, [_vp, _u8p, _szp, _sz, _u8p, _szp, _sz, _u8p]),
+    ("ovh_aggregate_pks", ctypes.c_int, [_vp, _u8p, _szp, _sz, _u8p]),
+    ("ovh_verify_aggregated", ctypes.c_int, [_vp, _u8p, _sz, _u8p, _sz, _u8p, _szp, _sz]),
+    ("ovh_verify_batch", ctypes.c_int, [_vp, _sz, _u8p, _u8p, _u8p, ctypes.c_uint64, _vp]),
+    ("ovh_verify_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+    ("ovh_batch_partial_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
+    ("ovh_combine_partials_device", ctypes.c_int, [_vp, _sz, _vp]),
+    ("ovh_batch_fallback_device", ctypes.c_int, [_vp, _sz, _vp]),
+    ("ovh_sign_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp]),
+    ("ovh_sk_to_pk_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp]),
+]
+
+_lib = None
+
+
+def load():
+    """Load libovhip.so (raises OSError/RuntimeError if it is missing: no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            "libovhip.so not built (%s): run `make -C consensus_overlord_amd` or __graft_entry__.build()" % LIB_PATH)
+    # One HIP runtime per process: torch (ROCm wheel) bundles its own libamdhip64.so.7. If it
+    # is importable, load it first so libovhip's NEEDED libamdhip64.so.7 binds to that copy
+    # and torch tensors / RCCL and libovhip share device contexts. Without torch, libovhip
+    # binds to the system ROCm runtime (RUNPATH).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib

@@ -1,0 +1,187 @@
+"""Host-side mirror of the reference's `ConsensusCrypto` (src/consensus.rs:334-463) over the
+libovhip C ABI: same method names, argument meaning and error behaviour. Every method runs
+its arithmetic in HIP kernels on the context's MI355X (hash/SM3 runs on the host, as in the
+reference, util.rs:83-87).
+
+Errors mirror `ConsensusError` (src/error.rs:20-44): `Other(String)` for the hash-length,
+length-mismatch and "lose public key" cases, `CryptoErr(code)` for blst errors.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+
+OK = 0
+ERR_HASH_LEN = 100
+ERR_LEN_MISMATCH = 101
+ERR_PUBKEY = 102
+ERR_ARG = 103
+ERR_DEVICE = 200
+
+BLST_ERRORS = {
+    1: "BLST_BAD_ENCODING",
+    2: "BLST_POINT_NOT_ON_CURVE",
+    3: "BLST_POINT_NOT_IN_GROUP",
+    4: "BLST_AGGR_TYPE_MISMATCH",
+    5: "BLST_VERIFY_FAIL",
+    6: "BLST_PK_IS_INFINITY",
+    7: "BLST_BAD_SCALAR",
+}
+
+
+class ConsensusError(Exception):
+    """src/error.rs:20 ConsensusError."""
+
+
+class Other(ConsensusError):
+    """ConsensusError::Other(String)."""
+
+
+class CryptoErr(ConsensusError):
+    """ConsensusError::CryptoErr(Box<ophelia::Error>)."""
+
+    def __init__(self, code: int):
+        super().__init__("Crypto error %s" % BLST_ERRORS.get(code, code))
+        self.code = code
+
+
+class DeviceError(ConsensusError):
+    pass
+
+
+def raise_for(code: int) -> None:
+    if code == OK:
+        return
+    if code == ERR_HASH_LEN:
+        raise Other("failed to convert hash value")
+    if code == ERR_LEN_MISMATCH:
+        raise Other("signatures length does not match voters length")
+    if code == ERR_PUBKEY:
+        raise Other("lose public key")
+    if 1 <= code <= 7:
+        raise CryptoErr(code)
+    if code == ERR_ARG:
+        raise ValueError("invalid argument")
+    raise DeviceError("libovhip device error (code %d)" % code)
+
+
+def _concat(items: Sequence[bytes]):
+    items = [bytes(x) for x in items]
+    lens = (ctypes.c_size_t * max(1, len(items)))(*[len(x) for x in items])
+    return b"".join(items), lens
+
+
+class Context:
+    """One libovhip context (device memory, stream, DST) on HIP device `device`."""
+
+    def __init__(self, device: int = 0, dst: Optional[bytes] = None, flags: int = 0):
+        self.lib = _lib.load()
+        d = None if dst is None else bytes(dst)
+        self.ptr = self.lib.ovh_create(device, d, 0 if d is None else len(d), flags)
+        if not self.ptr:
+            raise DeviceError("ovh_create failed on device %d (no usable MI355X?)" % device)
+        self.device = device
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self.lib.ovh_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return self.lib.ovh_stream(self.ptr)
+
+
+class ConsensusCrypto:
+    """Mirror of `ConsensusCrypto` / overlord's `Crypto` trait (consensus.rs:339-463)."""
+
+    def __init__(self, private_key: bytes, device: int = 0, dst: Optional[bytes] = None, ctx: Optional[Context] = None):
+        """consensus.rs:347-359 `new`: private key = 32-byte scalar (hex text or raw bytes);
+        name = the 48-byte compressed public key; common_ref = ''."""
+        if isinstance(private_key, str):
+            private_key = bytes.fromhex(private_key.strip())
+        self.ctx = ctx if ctx is not None else Context(device, dst)
+        self.lib = self.ctx.lib
+        self.private_key = bytes(private_key)
+        self.common_ref = ""
+        out = ctypes.create_string_buffer(48)
+        raise_for(self.lib.ovh_sk_to_pk(self.ctx.ptr, self.private_key, len(self.private_key), out))
+        self.name = out.raw
+        self.pubkeys: List[bytes] = []
+
+    @classmethod
+    def from_key_file(cls, path: str, **kw) -> "ConsensusCrypto":
+        with open(path) as fh:
+            return cls(bytes.fromhex(fh.read().strip()), **kw)
+
+    def update_pubkeys(self, new_pubkeys: Sequence[bytes]) -> None:
+        """consensus.rs:361-363."""
+        self.pubkeys = [bytes(p) for p in new_pubkeys]
+
+    # ---- overlord::Crypto ----
+    def hash(self, msg: bytes) -> bytes:
+        """consensus.rs:386-388 -> util.rs:83-87 (SM3)."""
+        msg = bytes(msg)
+        out = ctypes.create_string_buffer(32)
+        raise_for(self.lib.ovh_sm3(msg, len(msg), out))
+        return out.raw
+
+    def sign(self, hash_: bytes) -> bytes:
+        """consensus.rs:390-395."""
+        hash_ = bytes(hash_)
+        out = ctypes.create_string_buffer(96)
+        raise_for(self.lib.ovh_sign(self.ctx.ptr, self.private_key, len(self.private_key), hash_, len(hash_), out))
+        return out.raw
+
+    def verify_signature(self, signature: bytes, hash_: bytes, voter: bytes) -> None:
+        """consensus.rs:397-416."""
+        s, h, v = bytes(signature), bytes(hash_), bytes(voter)
+        raise_for(self.lib.ovh_verify(self.ctx.ptr, s, len(s), h, len(h), v, len(v)))
+
+    def aggregate_signatures(self, signatures: Sequence[bytes], voters: Sequence[bytes]) -> bytes:
+        """consensus.rs:418-444."""
+        sd, sl = _concat(signatures)
+        vd, vl = _concat(voters)
+        out = ctypes.create_string_buffer(96)
+        raise_for(self.lib.ovh_aggregate_sigs(self.ctx.ptr, sd, sl, len(signatures), vd, vl, len(voters), out))
+        return out.raw
+
+    def verify_aggregated_signature(self, aggregated_signature: bytes, hash_: bytes, voters: Sequence[bytes]) -> None:
+        """consensus.rs:446-462."""
+        a, h = bytes(aggregated_signature), bytes(hash_)
+        vd, vl = _concat(voters)
+        raise_for(self.lib.ovh_verify_aggregated(self.ctx.ptr, a, len(a), h, len(h), vd, vl, len(voters)))
+
+    # ---- extensions ----
+    def aggregate_public_keys(self, voters: Sequence[bytes]) -> bytes:
+        """BlsPublicKey::aggregate (consensus.rs:371) -> 48-byte compressed."""
+        vd, vl = _concat(voters)
+        out = ctypes.create_string_buffer(48)
+        raise_for(self.lib.ovh_aggregate_pks(self.ctx.ptr, vd, vl, len(voters), out))
+        return out.raw
+
+    def verify_batch(self, signatures, hashes, voters, seed: int = 0) -> np.ndarray:
+        """Batched verify_signature: returns int32 codes[n], codes[i] == the ovh_verify result
+        for vote i (0 = Ok). Fixed-size inputs: 96-byte sigs, 32-byte hashes, 48-byte pks."""
+        n = len(signatures)
+        if not (len(hashes) == len(voters) == n):
+            raise ValueError("batch lists must have equal length")
+        sig = b"".join(bytes(s) for s in signatures)
+        hs = b"".join(bytes(h) for h in hashes)
+        pk = b"".join(bytes(v) for v in voters)
+        if len(sig) != 96 * n or len(hs) != 32 * n or len(pk) != 48 * n:
+            raise ValueError("verify_batch takes 96-byte signatures, 32-byte hashes, 48-byte voters")
+        codes = np.zeros(max(n, 1), dtype=np.int32)
+        raise_for(self.lib.ovh_verify_batch(self.ctx.ptr, n, sig, hs, pk, seed & 0xFFFFFFFFFFFFFFFF,
+                                            codes.ctypes.data_as(ctypes.c_void_p)))
+        return codes[:n]

@@ -1,0 +1,62 @@
+"""Device-resident batch entry points (HBM in, HBM out). torch provides the device memory
+only; every kernel is libovhip's. The library runs on its own HIP stream and returns after
+its work completed, so callers synchronise torch's stream before handing buffers over."""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from .crypto import Context, raise_for
+
+
+def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
+    assert t.is_cuda and t.is_contiguous()
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def sk_to_pk_batch(ctx: Context, sks: torch.Tensor) -> torch.Tensor:
+    """sks: (n, 32) uint8 on device -> (n, 48) compressed pks."""
+    n = sks.shape[0]
+    out = torch.empty((n, 48), dtype=torch.uint8, device=sks.device)
+    torch.cuda.synchronize(sks.device)
+    raise_for(ctx.lib.ovh_sk_to_pk_batch_device(ctx.ptr, n, _ptr(sks), _ptr(out)))
+    return out
+
+
+def sign_batch(ctx: Context, sks: torch.Tensor, hashes: torch.Tensor) -> torch.Tensor:
+    n = sks.shape[0]
+    out = torch.empty((n, 96), dtype=torch.uint8, device=sks.device)
+    torch.cuda.synchronize(sks.device)
+    raise_for(ctx.lib.ovh_sign_batch_device(ctx.ptr, n, _ptr(sks), _ptr(hashes), _ptr(out)))
+    return out
+
+
+def verify_batch(ctx: Context, sigs: torch.Tensor, hashes: torch.Tensor, pks: torch.Tensor, seed: int,
+                 codes: torch.Tensor = None) -> torch.Tensor:
+    n = sigs.shape[0]
+    if codes is None:
+        codes = torch.empty((n,), dtype=torch.int32, device=sigs.device)
+    raise_for(ctx.lib.ovh_verify_batch_device(ctx.ptr, n, _ptr(sigs), _ptr(hashes), _ptr(pks),
+                                              seed & 0xFFFFFFFFFFFFFFFF, _ptr(codes)))
+    return codes
+
+
+def batch_partial(ctx: Context, sigs, hashes, pks, seed: int, codes: torch.Tensor, partial: torch.Tensor) -> None:
+    """Per-shard partial (864 bytes: Fp12 Miller product + Jacobian G2 sum) into `partial`."""
+    n = sigs.shape[0]
+    raise_for(ctx.lib.ovh_batch_partial_device(ctx.ptr, n, _ptr(sigs), _ptr(hashes), _ptr(pks),
+                                               seed & 0xFFFFFFFFFFFFFFFF, _ptr(codes), _ptr(partial)))
+
+
+def combine_partials(ctx: Context, partials: torch.Tensor) -> bool:
+    """partials: (k, 864) uint8 on device -> combined check passed?"""
+    k = partials.shape[0]
+    r = ctx.lib.ovh_combine_partials_device(ctx.ptr, k, _ptr(partials))
+    if r < 0:
+        raise_for(-r)
+    return r == 1
+
+
+def batch_fallback(ctx: Context, n: int, codes: torch.Tensor) -> None:
+    raise_for(ctx.lib.ovh_batch_fallback_device(ctx.ptr, n, _ptr(codes)))

@@ -1,0 +1,84 @@
+// Host build of the DEVICE arithmetic (consensus_overlord_amd/csrc/bls/*.hpp) for CPU unit
+// tests against the golden fixtures. Test infrastructure only: never linked into the
+// product library, never a fallback.
+#include <string.h>
+#include "../../consensus_overlord_amd/csrc/bls/verify.hpp"
+
+using namespace ovh;
+
+static const uint8_t DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_";
+
+extern "C" {
+
+int hx_hash_to_g2(const uint8_t* msg32, const uint8_t* dst, uint32_t dst_len, uint8_t* out192) {
+  XmdTemplates t;
+  if (!xmd_build_templates(t, dst, dst_len)) return -1;
+  uint32_t m[8];
+  be_words_from_bytes(m, msg32, 8);
+  G2J h;
+  hash_to_g2(h, m, t);
+  g2_serialize(out192, h);
+  return 0;
+}
+
+int hx_verify(const uint8_t* sig, uint32_t sl, const uint8_t* hash, uint32_t hl, const uint8_t* pk, uint32_t pl) {
+  XmdTemplates t;
+  xmd_build_templates(t, DST, 43);
+  return verify_one(sig, sl, hash, hl, pk, pl, t);
+}
+
+int hx_g1_decode(const uint8_t* in, uint32_t len, uint8_t* out48, int* inf) {
+  G1A a;
+  bool i;
+  int e = g1_from_bytes(a, i, in, len);
+  *inf = i;
+  if (e == 0) {
+    G1J j;
+    if (i) jac_set_inf(j); else jac_from_aff(j, a);
+    g1_compress(out48, j);
+  }
+  return e;
+}
+
+int hx_g2_decode(const uint8_t* in, uint32_t len, uint8_t* out96, int* inf) {
+  G2A a;
+  bool i;
+  int e = g2_from_bytes(a, i, in, len);
+  *inf = i;
+  if (e == 0) {
+    G2J j;
+    if (i) jac_set_inf(j); else jac_from_aff(j, a);
+    g2_compress(out96, j);
+  }
+  return e;
+}
+
+// e(G1, G2)^3 via the device Miller loop + x-chain final exponentiation; 12 Fp2 coeffs
+// (c0.c0.c0, c0.c0.c1, c0.c1.c0, ...) as 48-byte BE canonical values.
+void hx_gt_g1g2(uint8_t* out576) {
+  G1A p; fp_load(p.x, G1X_M); fp_load(p.y, G1Y_M);
+  G2A q; q.x = fp2_const(G2X_C0, G2X_C1); q.y = fp2_const(G2Y_C0, G2Y_C1);
+  Fp12 f;
+  miller_loop(f, p, q);
+  final_exponentiation(f, f);
+  const Fp* c = &f.c0.c0.c0;
+  for (int i = 0; i < 12; ++i) fp_to_be48(out576 + 48 * i, c[i]);
+}
+
+int hx_g2_subgroup(const uint8_t* in, uint32_t len) {
+  G2A a; bool i;
+  int e = g2_from_bytes(a, i, in, len);
+  if (e) return -e;
+  G2J j; jac_from_aff(j, a);
+  return g2_in_subgroup(j) ? 1 : 0;
+}
+
+int hx_g1_subgroup(const uint8_t* in, uint32_t len) {
+  G1A a; bool i;
+  int e = g1_from_bytes(a, i, in, len);
+  if (e) return -e;
+  G1J j; jac_from_aff(j, a);
+  return g1_in_subgroup(j) ? 1 : 0;
+}
+
+}

@@ -1,0 +1,176 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle's golden fixtures and
+against the Python oracle on seeded inputs. Bit-exact: verdicts, error codes and
+aggregated signature / public key bytes."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cc():
+    import consensus_overlord_amd as coa
+    return coa.ConsensusCrypto(bytes.fromhex("11" * 32))
+
+
+def _b(h):
+    return bytes.fromhex(h)
+
+
+def _code(fn):
+    from consensus_overlord_amd.crypto import ConsensusError, CryptoErr, Other
+    try:
+        fn()
+        return 0
+    except CryptoErr as e:
+        return e.code
+    except Other as e:
+        return {"failed to convert hash value": 100,
+                "signatures length does not match voters length": 101,
+                "lose public key": 102}[str(e)]
+
+
+def test_verify_golden_exact_codes(cc, golden):
+    for c in golden["verify"]:
+        got = cc.lib.ovh_verify(cc.ctx.ptr, _b(c["sig"]), len(_b(c["sig"])), _b(c["hash"]), len(_b(c["hash"])),
+                                _b(c["pk"]), len(_b(c["pk"])))
+        assert got == c["code"], c["name"]
+
+
+def test_trait_error_mapping(cc, golden):
+    by = {c["name"]: c for c in golden["verify"]}
+    for name, code in (("valid_0", 0), ("hash_31", 100), ("pk_47", 102), ("sig_95", 1), ("wrong_msg", 5)):
+        c = by[name]
+        assert _code(lambda: cc.verify_signature(_b(c["sig"]), _b(c["hash"]), _b(c["pk"]))) == code
+
+
+def test_sign_and_pubkey_golden(golden):
+    import consensus_overlord_amd as coa
+    for k, v in zip(golden["keys"][:4], golden["votes"][:4]):
+        c = coa.ConsensusCrypto(_b(k["sk"]))
+        assert c.name.hex() == k["pk"]
+        assert c.sign(_b(v["digest"])).hex() == v["sig"]
+        assert c.hash(_b(v["rlp"])).hex() == v["digest"]
+
+
+def test_aggregate_golden(cc, golden):
+    for c in golden["aggregate"]:
+        sigs = [_b(s) for s in c["sigs"]]
+        pks = [_b(p) for p in c["pks"]]
+        out = {}
+
+        def run():
+            out["v"] = cc.aggregate_signatures(sigs, pks)
+        code = _code(run)
+        assert code == c["code"], c["name"]
+        if code == 0:
+            assert out["v"].hex() == c["out"], c["name"]
+    for c in golden["aggregate_pks"]:
+        pks = [_b(p) for p in c["pks"]]
+        out = {}
+
+        def run():
+            out["v"] = cc.aggregate_public_keys(pks)
+        code = _code(run)
+        assert code == c["code"], c["name"]
+        if code == 0:
+            assert out["v"].hex() == c["out"], c["name"]
+
+
+def test_qc_config2(cc, golden):
+    q = golden["qc"]
+    pks = [_b(p) for p in q["pks"]]
+    sigs = [_b(s) for s in q["sigs"]]
+    h = _b(q["hash"])
+    assert cc.aggregate_signatures(sigs, pks[:67]).hex() == q["agg_sig"]
+    assert cc.aggregate_public_keys(pks[:67]).hex() == q["agg_pk"]
+    agg = _b(q["agg_sig"])
+    assert _code(lambda: cc.verify_aggregated_signature(agg, h, pks[:67])) == q["verify_ok"]
+    assert _code(lambda: cc.verify_aggregated_signature(agg, h, pks[:66])) == q["verify_missing_one"]
+    assert _code(lambda: cc.verify_aggregated_signature(agg, _b("00" * 32), pks[:67])) == 5
+    assert _code(lambda: cc.verify_aggregated_signature(agg, h, [])) == q["verify_empty"]
+    assert _code(lambda: cc.verify_aggregated_signature(agg, h[:31], pks[:67])) == q["verify_hash_31"]
+    assert _code(lambda: cc.verify_aggregated_signature(agg, h, pks[:66] + [pks[0][:40]])) == q["verify_bad_pk"]
+
+
+def test_batch_matches_per_vote_golden(cc, golden):
+    # every fixed-size golden case (96/32/48 bytes) through the batch path == per-vote code
+    cases = [c for c in golden["verify"] if len(_b(c["sig"])) == 96 and len(_b(c["hash"])) == 32
+             and len(_b(c["pk"])) == 48]
+    codes = cc.verify_batch([_b(c["sig"]) for c in cases], [_b(c["hash"]) for c in cases],
+                            [_b(c["pk"]) for c in cases], seed=7)
+    for c, got in zip(cases, codes):
+        assert got == c["code"], c["name"]
+
+
+def test_batch_all_valid_uses_rlc(cc, golden):
+    v = golden["votes"]
+    k = golden["keys"]
+    codes = cc.verify_batch([_b(x["sig"]) for x in v], [_b(x["digest"]) for x in v], [_b(x["pk"]) for x in k], seed=1)
+    assert list(codes) == [0] * len(v)
+
+
+def _synth(n, seed=0xC17A):
+    import torch
+    import overlord_oracle as ov
+    sks = np.zeros((n, 32), dtype=np.uint8)
+    hs = np.zeros((n, 32), dtype=np.uint8)
+    for i in range(n):
+        sks[i] = np.frombuffer(ov.synth_sk(i, seed).to_bytes(32, "big"), dtype=np.uint8)
+        hs[i] = np.frombuffer(hashlib.sha256(b"vote%d" % i).digest(), dtype=np.uint8)
+    return torch.from_numpy(sks).cuda(), torch.from_numpy(hs).cuda()
+
+
+def test_device_batch_config5_invalid_positions(cc):
+    """Config 5 shape at n = 256: 1% invalid (sigma replaced by sigma + G2) at seeded random
+    positions; every invalid position flagged (code 5), every other vote Ok."""
+    import torch
+    import bls12_381 as bls
+    from consensus_overlord_amd import device as dev
+    n = 256
+    sks, hs = _synth(n)
+    pks = dev.sk_to_pk_batch(cc.ctx, sks)
+    sigs = dev.sign_batch(cc.ctx, sks, hs)
+    # oracle spot-check of device signing/pk derivation
+    rng = random.Random(3)
+    for i in rng.sample(range(n), 3):
+        sk = int.from_bytes(sks[i].cpu().numpy().tobytes(), "big")
+        assert bytes(pks[i].cpu().numpy()) == bls.g1_compress(bls.sk_to_pk(sk))
+        assert bytes(sigs[i].cpu().numpy()) == bls.g2_compress(bls.sign(sk, bytes(hs[i].cpu().numpy())))
+    bad = sorted(rng.sample(range(n), max(1, n // 100)))
+    s_host = sigs.cpu().numpy().copy()
+    for i in bad:
+        pt = bls.g2_from_bytes(bytes(s_host[i]))
+        s_host[i] = np.frombuffer(bls.g2_compress(bls.pt_add(bls.Fp2Ops, pt, bls.G2_GEN)), dtype=np.uint8)
+    sigs2 = torch.from_numpy(s_host).cuda()
+    torch.cuda.synchronize()
+    codes = dev.verify_batch(cc.ctx, sigs2, hs, pks, seed=99).cpu().numpy()
+    assert [i for i in range(n) if codes[i] != 0] == bad
+    assert all(codes[i] == 5 for i in bad)
+    codes = dev.verify_batch(cc.ctx, sigs, hs, pks, seed=100).cpu().numpy()
+    assert (codes == 0).all()
+
+
+def test_partials_combine_two_shards(cc):
+    import torch
+    from consensus_overlord_amd import device as dev
+    n = 128
+    sks, hs = _synth(n, seed=5)
+    pks = dev.sk_to_pk_batch(cc.ctx, sks)
+    sigs = dev.sign_batch(cc.ctx, sks, hs)
+    parts = torch.empty((2, 864), dtype=torch.uint8, device="cuda")
+    codes = torch.empty((n,), dtype=torch.int32, device="cuda")
+    h = n // 2
+    dev.batch_partial(cc.ctx, sigs[:h], hs[:h], pks[:h], 11, codes[:h], parts[0])
+    dev.batch_partial(cc.ctx, sigs[h:], hs[h:], pks[h:], 12, codes[h:], parts[1])
+    assert dev.combine_partials(cc.ctx, parts)
+    # swap two hashes across shards: the combined check must fail
+    hs2 = hs.clone()
+    hs2[[0, h]] = hs[[h, 0]]
+    torch.cuda.synchronize()
+    dev.batch_partial(cc.ctx, sigs[:h], hs2[:h], pks[:h], 11, codes[:h], parts[0])
+    dev.batch_partial(cc.ctx, sigs[h:], hs2[h:], pks[h:], 12, codes[h:], parts[1])
+    assert not dev.combine_partials(cc.ctx, parts)
