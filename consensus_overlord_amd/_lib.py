@@ -30,6 +30,8 @@ SIGNATURES = [
     ("ovh_batch_partial_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     ("ovh_combine_partials_device", ctypes.c_int, [_vp, _sz, _vp]),
     ("ovh_batch_fallback_device", ctypes.c_int, [_vp, _sz, _vp]),
+    ("ovh_stage_times", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_float), _sz]),
+    ("ovh_stage_name", ctypes.c_char_p, [ctypes.c_int]),
     ("ovh_sign_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp]),
     ("ovh_sk_to_pk_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp]),
 ]

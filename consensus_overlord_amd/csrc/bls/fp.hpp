@@ -27,6 +27,14 @@
 
 namespace ovh {
 
+// Host-only op counter for the work model (tools/count_muls.cpp); compiled out everywhere else.
+#if defined(OVH_COUNT_MULS) && !defined(__HIP_DEVICE_COMPILE__)
+extern unsigned long long g_fp_mul_count;
+#define OVH_COUNT_MUL() (++::ovh::g_fp_mul_count)
+#else
+#define OVH_COUNT_MUL() ((void)0)
+#endif
+
 // 32-bit add/sub with carry: clang lowers the builtins to v_add_co/v_addc_co chains.
 OVH_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t cin, uint32_t* cout) {
 #if defined(__clang__)
@@ -125,6 +133,7 @@ OVH_HD void fp_mul(Fp& r, const Fp& a, const Fp& b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   fp_mul_gfx950(r.v, a.v, b.v);
 #else
+  OVH_COUNT_MUL();
   uint32_t t[12];
 #pragma unroll
   for (int j = 0; j < 12; ++j) t[j] = 0;

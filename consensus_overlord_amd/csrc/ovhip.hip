@@ -101,6 +101,12 @@ enum : uint32_t {
   S_TOTAL = 46,
 };
 
+enum : int {
+  ST_PARSE_PK = 0, ST_PARSE_SIG, ST_CODES, ST_H2F, ST_SSWU, ST_H2C_FIN,
+  ST_SCALAR, ST_MILLER, ST_REDUCE, ST_FINAL, ST_FALLBACK,
+};
+static_assert(ST_FALLBACK + 1 == OVH_NSTAGES, "stage table");
+
 __device__ __forceinline__ uint64_t rlc_scalar(uint64_t seed, uint32_t i) {
   // SplitMix64 on (seed, i): the 64-bit RLC coefficient of vote i (never 0).
   uint64_t z = seed + 0x9e3779b97f4a7c15ull * ((uint64_t)i + 1);
@@ -505,6 +511,28 @@ struct ovh_ctx {
   uint32_t* partial = nullptr;   // 216 words
   int32_t* result = nullptr;     // device scalar
   uint32_t last_n = 0;
+  // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
+  hipEvent_t ev0[OVH_NSTAGES] = {}, ev1[OVH_NSTAGES] = {};
+  uint32_t ev_mask = 0;
+};
+
+static const char* const STAGE_NAMES[OVH_NSTAGES] = {
+    "parse_pk", "parse_sig", "codes", "hash_to_field", "sswu_iso", "h2c_finish",
+    "rlc_scalar", "miller", "reduce", "final", "fallback"};
+
+// Stage bracket: events on the context's stream around the stage's kernels.
+struct StageScope {
+  ovh_ctx* c;
+  int k;
+  StageScope(ovh_ctx* c_, int k_) : c(c_), k(k_) {
+    if (c->flags & OVH_FLAG_PROFILE) (void)hipEventRecord(c->ev0[k], c->stream);
+  }
+  ~StageScope() {
+    if (c->flags & OVH_FLAG_PROFILE) {
+      (void)hipEventRecord(c->ev1[k], c->stream);
+      c->ev_mask |= 1u << k;
+    }
+  }
 };
 
 #define HIPCHK(x)                                  \
@@ -567,6 +595,12 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
     delete c;
     return nullptr;
   }
+  if (flags & OVH_FLAG_PROFILE)
+    for (int k = 0; k < OVH_NSTAGES; ++k)
+      if (hipEventCreate(&c->ev0[k]) != hipSuccess || hipEventCreate(&c->ev1[k]) != hipSuccess) {
+        ovh_destroy(c);
+        return nullptr;
+      }
   return c;
 }
 
@@ -578,8 +612,28 @@ void ovh_destroy(ovh_ctx* c) {
                   (void*)c->in_buf, (void*)c->partial, (void*)c->result})
     if (p) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  for (int k = 0; k < OVH_NSTAGES; ++k) {
+    if (c->ev0[k]) (void)hipEventDestroy(c->ev0[k]);
+    if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
+  }
   delete c;
 }
+
+int ovh_stage_times(ovh_ctx* c, float* ms, size_t max) {
+  if (!c || (!ms && max)) return -OVH_ERR_ARG;
+  if (!(c->flags & OVH_FLAG_PROFILE)) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) return -OVH_ERR_DEVICE;
+  const size_t n = max < OVH_NSTAGES ? max : OVH_NSTAGES;
+  for (size_t k = 0; k < n; ++k) {
+    ms[k] = 0.f;
+    if (c->ev_mask & (1u << k))
+      if (hipEventElapsedTime(&ms[k], c->ev0[k], c->ev1[k]) != hipSuccess) return -OVH_ERR_DEVICE;
+  }
+  return (int)n;
+}
+
+const char* ovh_stage_name(int k) { return (k >= 0 && k < OVH_NSTAGES) ? STAGE_NAMES[k] : nullptr; }
 
 void* ovh_stream(ovh_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
@@ -807,34 +861,37 @@ static int batch_front(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint
   Slab s{c->state, c->cap};
   Slab sig{c->state + (size_t)S_SIG * 12 * c->cap, c->cap};
   hipStream_t st = c->stream;
-  k_parse_pk<<<nblk(n), WG, 0, st>>>(n, d_pks, c->st_pk, s);
-  k_parse_sig<<<nblk(n), WG, 0, st>>>(n, d_sigs, c->st_sig, sig);
-  k_codes<<<nblk(n), WG, 0, st>>>(n, c->st_pk, c->st_sig, d_codes);
-  k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s);
-  k_sswu<<<nblk(2 * (size_t)n), WG, 0, st>>>(n, s);
-  k_h2c_fin<<<nblk(n), WG, 0, st>>>(n, s, d_codes);
-  k_scalar<<<nblk(n), WG, 0, st>>>(n, seed, s, d_codes);
-  k_miller<<<nblk(n), WG, 0, st>>>(n, s, d_codes);
+  c->ev_mask = 0;
+  { StageScope p(c, ST_PARSE_PK); k_parse_pk<<<nblk(n), WG, 0, st>>>(n, d_pks, c->st_pk, s); }
+  { StageScope p(c, ST_PARSE_SIG); k_parse_sig<<<nblk(n), WG, 0, st>>>(n, d_sigs, c->st_sig, sig); }
+  { StageScope p(c, ST_CODES); k_codes<<<nblk(n), WG, 0, st>>>(n, c->st_pk, c->st_sig, d_codes); }
+  { StageScope p(c, ST_H2F); k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s); }
+  { StageScope p(c, ST_SSWU); k_sswu<<<nblk(2 * (size_t)n), WG, 0, st>>>(n, s); }
+  { StageScope p(c, ST_H2C_FIN); k_h2c_fin<<<nblk(n), WG, 0, st>>>(n, s, d_codes); }
+  { StageScope p(c, ST_SCALAR); k_scalar<<<nblk(n), WG, 0, st>>>(n, seed, s, d_codes); }
+  { StageScope p(c, ST_MILLER); k_miller<<<nblk(n), WG, 0, st>>>(n, s, d_codes); }
   HIPCHK(hipGetLastError());
   // reductions
   const uint32_t chunk = 16;
   Slab fin{c->state + (size_t)S_F * 12 * c->cap, c->cap};
   Slab sin{c->state + (size_t)S_RS * 12 * c->cap, c->cap};
-  uint32_t m = n;
-  int flip = 0;
-  while (m > 1) {
-    const uint32_t mo = (m + chunk - 1) / chunk;
-    uint32_t* base = c->red + (size_t)flip * 18 * 12 * c->red_cap;
-    Slab fo{base, c->red_cap}, so{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
-    k_reduce_f<<<nblk(mo), WG, 0, st>>>(m, chunk, fin, fo);
-    k_reduce_s<<<nblk(mo), WG, 0, st>>>(m, chunk, sin, so);
-    fin = fo;
-    sin = so;
-    m = mo;
-    flip ^= 1;
+  {
+    StageScope p(c, ST_REDUCE);
+    uint32_t m = n;
+    int flip = 0;
+    while (m > 1) {
+      const uint32_t mo = (m + chunk - 1) / chunk;
+      uint32_t* base = c->red + (size_t)flip * 18 * 12 * c->red_cap;
+      Slab fo{base, c->red_cap}, so{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
+      k_reduce_f<<<nblk(mo), WG, 0, st>>>(m, chunk, fin, fo);
+      k_reduce_s<<<nblk(mo), WG, 0, st>>>(m, chunk, sin, so);
+      fin = fo;
+      sin = so;
+      m = mo;
+      flip ^= 1;
+    }
+    k_pack_partial<<<1, WG, 0, st>>>(fin, sin, c->partial);
   }
-  HIPCHK(hipGetLastError());
-  k_pack_partial<<<1, WG, 0, st>>>(fin, sin, c->partial);
   HIPCHK(hipGetLastError());
   c->last_n = n;
   return 0;
@@ -867,7 +924,10 @@ int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials)
   if (!c || !d_partials || k == 0 || k > 4096) return -OVH_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return -OVH_ERR_DEVICE;
-  k_final<<<1, WG, 0, c->stream>>>((uint32_t)k, (const uint32_t*)d_partials, c->result);
+  {
+    StageScope p(c, ST_FINAL);
+    k_final<<<1, WG, 0, c->stream>>>((uint32_t)k, (const uint32_t*)d_partials, c->result);
+  }
   if (hipGetLastError() != hipSuccess) return -OVH_ERR_DEVICE;
   int32_t r = -1;
   if (hipMemcpyAsync(&r, c->result, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return -OVH_ERR_DEVICE;
@@ -882,7 +942,10 @@ int ovh_batch_fallback_device(ovh_ctx* c, size_t n, int32_t* d_codes) {
   if (n == 0) return 0;
   if (n != c->last_n) return OVH_ERR_ARG;
   Slab s{c->state, c->cap};
-  k_fallback<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, s, d_codes);
+  {
+    StageScope p(c, ST_FALLBACK);
+    k_fallback<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, s, d_codes);
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
@@ -897,13 +960,17 @@ int ovh_verify_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const u
   if (ensure_cap(c, n)) return OVH_ERR_DEVICE;
   int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes);
   if (e) return e;
-  k_final<<<1, WG, 0, c->stream>>>(1, c->partial, c->result);
+  {
+    StageScope p(c, ST_FINAL);
+    k_final<<<1, WG, 0, c->stream>>>(1, c->partial, c->result);
+  }
   HIPCHK(hipGetLastError());
   int32_t r = -1;
   HIPCHK(hipMemcpyAsync(&r, c->result, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (r != 1) {
     Slab s{c->state, c->cap};
+    StageScope p(c, ST_FALLBACK);
     k_fallback<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, s, d_codes);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));

@@ -40,6 +40,11 @@ typedef struct ovh_ctx ovh_ctx;
 
 /* Flags for ovh_create. */
 #define OVH_FLAG_AGG_NO_GROUPCHECK 0x1u /* aggregate_signatures without the G2 subgroup check */
+#define OVH_FLAG_PROFILE 0x2u           /* record HIP events around every batch stage */
+
+/* Batch stages (ovh_stage_name gives the label). Each stage is one or more kernels enqueued
+ * back to back on ovh_stream. */
+#define OVH_NSTAGES 11
 
 /* Create a context on HIP device `device` with hash-to-curve domain separation tag `dst`
  * (NULL -> "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_", the believed ophelia-blst DST).
@@ -98,6 +103,14 @@ int ovh_combine_partials_device(ovh_ctx* ctx, size_t k, const uint8_t* d_partial
 /* Per-vote fallback for a shard whose combined check failed: codes[i] (device) updated to the
  * exact per-vote verify result for every vote whose code is still 0. */
 int ovh_batch_fallback_device(ovh_ctx* ctx, size_t n, int32_t* d_codes);
+
+/* Device time (ms, HIP events on ovh_stream) of each stage of the most recent batch call
+ * (ovh_verify_batch_device / ovh_batch_partial_device / ovh_combine_partials_device /
+ * ovh_batch_fallback_device) on a context created with OVH_FLAG_PROFILE; stages that did not
+ * run read 0. Fills min(max, OVH_NSTAGES) entries and returns that count (0 without the
+ * flag, <0 on error). */
+int ovh_stage_times(ovh_ctx* ctx, float* ms, size_t max);
+const char* ovh_stage_name(int stage);
 
 /* Batched helpers used to synthesise workloads on the device. */
 int ovh_sign_batch_device(ovh_ctx* ctx, size_t n, const uint8_t* d_sks, const uint8_t* d_hashes, uint8_t* d_sigs);

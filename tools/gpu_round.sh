@@ -1,0 +1,16 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, smoke, bench, rocprofv3 kernel stats. Every GPU step has its
+# own time limit; the first failure ends the script (set -e).
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+OUT=$R/gpurun_out/${TAG:-r01}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 300 python -c "import torch; print(torch.__version__, torch.cuda.is_available())" > "$OUT/torch.log" 2>&1
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+timeout -k 10 300 python -u bench.py --steps ${STEPS:-10} --warmup 2 > "$OUT/bench.log" 2>&1
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench -- python3 "$R/bench.py" --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline > "$OUT/bench_prof.log" 2>&1
+echo done > "$OUT/ok"
