@@ -46,10 +46,10 @@ OVH_FLAG_PROFILE = 0x2
 # (256 CU x 4 SIMD x 32 lanes x 2.4 GHz).
 PEAK_MAD_U64 = 2.9143e13
 PEAK_FULLRATE = 256 * 4 * 32 * 2.4e9
-STAGE_TO_WORK = {"parse_pk": "parse_pk", "parse_sig": "parse_sig", "hash_to_field": "hash_to_field",
-                 "sswu_iso": "sswu_iso", "h2c_finish": "h2c_finish", "rlc_scalar": "rlc_scalar",
-                 "miller": "miller", "reduce": "reduce", "final": "final_per_batch", "fallback": "fallback"}
+STAGE_TO_WORK = {"hash_to_field": "hash_to_field", "vote": "vote", "fold": "fold_per_partial",
+                 "final": "final_per_batch", "fallback": "fallback"}
 PER_BATCH_STAGES = {"final"}
+NSTAGES = 5
 
 
 def synth_inputs(lib, lo: int, n: int):
@@ -138,7 +138,7 @@ def main():
     partials = torch.empty((world, 864), dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
 
-    nst = 11
+    nst = NSTAGES
     names = [lib.ovh_stage_name(k).decode() for k in range(nst)]
     stage_ms = np.zeros(nst)
     buf = (ctypes.c_float * nst)()
@@ -198,9 +198,7 @@ def main():
         macs = Mu[STAGE_TO_WORK[dname]] * units * macs_per_M
         achieved = macs / (avg_ms[dom] * 1e-3) / 1e12
         value = world * B * args.steps / elapsed
-        path_M = sum(Mu[STAGE_TO_WORK[n]] for n in ("parse_pk", "parse_sig", "hash_to_field", "sswu_iso",
-                                                    "h2c_finish", "rlc_scalar", "miller", "reduce"))
-        path_M += Mu["final_per_batch"] / B
+        path_M = Mu["hash_to_field"] + Mu["vote"] + Mu["fold_per_partial"] * 4.0 / 3.0 + Mu["final_per_batch"] / B
         line = {
             "metric": "BLS12-381 vote verifications/sec (batch 4096) at 1/2/4/8 MI355X vs host blst",
             "value": round(value, 2),

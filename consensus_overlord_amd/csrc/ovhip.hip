@@ -1,19 +1,16 @@
 // libovhip: HIP (gfx950) implementation of the C ABI in include/ovhip.h.
 //
-// Batch verification data path (ovh_verify_batch_device), one lane per unit of work:
-//   k_parse_pk   vote i : pk decompress + G1 subgroup check        (consensus.rs:406)
-//   k_parse_sig  vote i : sig decompress + G2 subgroup check       (consensus.rs:409)
-//   k_codes      vote i : reference error precedence -> codes[i]
-//   k_h2f        vote i : expand_message_xmd + hash_to_field       (verify -> hash_to_G2)
-//   k_sswu       (vote, j) for j in {0,1}: SSWU + 3-isogeny
-//   k_h2c_fin    vote i : Q0 + Q1, clear cofactor, affine H_i
-//   k_scalar     vote i : r_i pk_i (affine), r_i sig_i (Jacobian), r_i from (seed, i)
-//   k_miller     vote i : f_i = Miller(r_i pk_i, H_i)
-//   k_reduce_*   chunked product of f_i / sum of r_i sig_i
-//   k_final      prod f_i * Miller(-G1, sum r_i sig_i) -> final exponentiation == 1 ?
-//   k_fallback   vote i : full per-vote pairing check when the combined check fails
+// Batch verification (ovh_verify_batch_device), DESIGN.md section 4:
+//   k_h2f         lane per vote: expand_message_xmd (SHA-256) + hash_to_field -> u0, u1
+//   k_vm_vote     16-lane slice per vote, 4 votes per wave: the Fp-VM "vote" program --
+//                 pk / sig decompression + subgroup checks, hash_to_G2, r pk, r sigma,
+//                 f = Miller(r pk, H); the epilogue writes the vote's code with the reference
+//                 precedence and its (f, r sigma) contribution (identity if the vote failed)
+//   k_vm_fold     16-lane slice per 4 partials: (prod f, sum S), repeated down to <= 4
+//   k_vm_final    one wave: prod f * Miller(-G1, sum S) -> final exponentiation == 1 ?
+//   k_vm_pairchk  16-lane slice per surviving vote when the combined check fails
 // Per-vote state lives in HBM as structure-of-arrays by limb: limb k of element i of an Fp
-// slab at slab[k * cap + i], so a wave's loads/stores are coalesced 256-byte lines.
+// plane j at slab[(j * 12 + k) * cap + i].
 #include <hip/hip_runtime.h>
 
 #include <mutex>
@@ -23,7 +20,9 @@
 
 #include "../../include/ovhip.h"
 #include "bls/verify.hpp"
+#include "fpvm.hpp"
 #include "sm3.hpp"
+#include "vm_progs.inc"
 
 using namespace ovh;
 
@@ -87,24 +86,18 @@ struct Slab {
   }
 };
 
-// Number of Fp slabs per vote region.
+// Fp planes of the per-vote state slab.
 enum : uint32_t {
-  S_PK = 0,     // 2 Fp: pk affine
-  S_RP = 2,     // 2 Fp: r * pk affine
-  S_SIG = 4,    // 4 Fp: sig affine
-  S_U = 8,      // 4 Fp: u0, u1
-  S_Q0 = 12,    // 6 Fp: SSWU/iso output 0 (Jacobian)
-  S_Q1 = 18,    // 6 Fp
-  S_H = 24,     // 4 Fp: H(m) affine
-  S_RS = 28,    // 6 Fp: r * sig (Jacobian)
-  S_F = 34,     // 12 Fp: Miller output
-  S_TOTAL = 46,
+  S_U = 0,      // 4 planes: u0, u1 (hash_to_field, Montgomery)
+  S_FB = 4,     // 12 planes: pk affine (2), sig affine (4), H projective (6) -- fallback inputs
+  S_RS = 16,    // 6 planes: r * sig (projective)
+  S_F = 22,     // 12 planes: f = Miller(r pk, H)
+  S_TOTAL = 34,
 };
+// partial = (F: 12 planes, S: 6 planes)
+constexpr uint32_t PART_PLANES = 18;
 
-enum : int {
-  ST_PARSE_PK = 0, ST_PARSE_SIG, ST_CODES, ST_H2F, ST_SSWU, ST_H2C_FIN,
-  ST_SCALAR, ST_MILLER, ST_REDUCE, ST_FINAL, ST_FALLBACK,
-};
+enum : int { ST_H2F = 0, ST_VOTE, ST_FOLD, ST_FINAL, ST_FALLBACK };
 static_assert(ST_FALLBACK + 1 == OVH_NSTAGES, "stage table");
 
 __device__ __forceinline__ uint64_t rlc_scalar(uint64_t seed, uint32_t i) {
@@ -117,64 +110,6 @@ __device__ __forceinline__ uint64_t rlc_scalar(uint64_t seed, uint32_t i) {
 }
 
 // ------------------------------------------------------------------------ kernels
-__global__ __launch_bounds__(WG) void k_parse_pk(uint32_t n, const uint8_t* __restrict__ pks, int32_t* __restrict__ st,
-                                                 Slab s) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  G1A a;
-  bool inf;
-  int e = g1_from_bytes(a, inf, pks + (size_t)i * 48, 48);
-  int code = 0;
-  if (e != BLST_SUCCESS) {
-    code = OVH_ERR_PUBKEY;
-  } else if (inf) {
-    code = BLST_PK_IS_INFINITY;
-  } else {
-    G1J j;
-    jac_from_aff(j, a);
-    if (!g1_in_subgroup(j)) code = BLST_POINT_NOT_IN_GROUP;
-  }
-  if (code == 0 || code == BLST_POINT_NOT_IN_GROUP) s.st_g1a(a, i);
-  st[i] = code;
-}
-
-#define SIG_INF_MARK 1000
-__global__ __launch_bounds__(WG) void k_parse_sig(uint32_t n, const uint8_t* __restrict__ sigs, int32_t* __restrict__ st,
-                                                  Slab s) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  G2A a;
-  bool inf;
-  int code = g2_from_bytes(a, inf, sigs + (size_t)i * 96, 96);
-  if (code == BLST_SUCCESS) {
-    if (inf) {
-      code = SIG_INF_MARK;
-    } else {
-      G2J j;
-      jac_from_aff(j, a);
-      if (!g2_in_subgroup(j)) code = BLST_POINT_NOT_IN_GROUP;
-      s.st_g2a(a, i);
-    }
-  }
-  st[i] = code;
-}
-
-// verify_signature precedence: pk parse (102) > sig parse (1..3) > sig group (3) >
-// pk infinity (6) > pk group (3) > [infinite sig -> pairing fails: 5] > pairing.
-__global__ __launch_bounds__(WG) void k_codes(uint32_t n, const int32_t* __restrict__ pk_st,
-                                              const int32_t* __restrict__ sig_st, int32_t* __restrict__ codes) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  const int p = pk_st[i], s = sig_st[i];
-  int c;
-  if (p == OVH_ERR_PUBKEY) c = OVH_ERR_PUBKEY;
-  else if (s != 0 && s != SIG_INF_MARK) c = s;
-  else if (p != 0) c = p;
-  else if (s == SIG_INF_MARK) c = BLST_VERIFY_FAIL;
-  else c = 0;
-  codes[i] = c;
-}
-
 __global__ __launch_bounds__(WG) void k_h2f(uint32_t n, const uint8_t* __restrict__ hashes, XmdTemplates t, Slab s) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n) return;
@@ -187,163 +122,256 @@ __global__ __launch_bounds__(WG) void k_h2f(uint32_t n, const uint8_t* __restric
   s.st2(u1, S_U + 2, i);
 }
 
-__global__ __launch_bounds__(WG) void k_sswu(uint32_t n, Slab s) {
-  const uint32_t t = blockIdx.x * WG + threadIdx.x;
-  if (t >= 2 * n) return;
-  const uint32_t i = t < n ? t : t - n;
-  const uint32_t j = t < n ? 0 : 1;
-  Fp2 u, x, y;
-  s.ld2(u, S_U + 2 * j, i);
-  map_to_curve_sswu(x, y, u);
-  G2J q;
-  iso_map_g2(q, x, y);
-  Slab o{s.p + (size_t)(j ? S_Q1 : S_Q0) * 12 * s.cap, s.cap};
-  o.st_g2j(q, i);
-}
-
-__global__ __launch_bounds__(WG) void k_h2c_fin(uint32_t n, Slab s, int32_t* __restrict__ codes) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  Slab q0{s.p + (size_t)S_Q0 * 12 * s.cap, s.cap}, q1{s.p + (size_t)S_Q1 * 12 * s.cap, s.cap};
-  G2J a, b;
-  q0.ld_g2j(a, i);
-  q1.ld_g2j(b, i);
-  jac_add(a, a, b);
-  g2_clear_cofactor(a, a);
-  G2A h;
-  if (!jac_to_aff(h, a)) {
-    if (codes[i] == 0) codes[i] = BLST_VERIFY_FAIL;  // H(m) = O (probability ~2^-255)
+// ZCash header of a compressed point without decompression (the VM program decompresses):
+// bad = BAD_ENCODING, inf = valid infinity encoding, x = masked plain limbs (x1 for G2).
+__device__ void parse_hdr(const uint8_t* b, uint32_t nbytes, uint32_t* x_hi, uint32_t* x_lo, uint32_t& bad,
+                          uint32_t& inf, uint32_t& sort, uint32_t& xzero) {
+  const uint8_t b0 = b[0];
+  bad = 0;
+  inf = 0;
+  sort = (b0 >> 5) & 1u;
+  xzero = 0;
+  uint8_t t[48];
+  for (int i = 0; i < 48; ++i) t[i] = b[i];
+  t[0] &= 0x1f;
+  limbs_from_be48(x_hi, t);
+  if (nbytes == 96) limbs_from_be48(x_lo, b + 48);
+  if (!(b0 & 0x80)) {
+    bad = 1;
     return;
   }
-  Slab o{s.p + (size_t)S_H * 12 * s.cap, s.cap};
-  o.st_g2a(h, i);
-}
-
-__global__ __launch_bounds__(WG) void k_scalar(uint32_t n, uint64_t seed, Slab s, const int32_t* __restrict__ codes) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  Slab rs{s.p + (size_t)S_RS * 12 * s.cap, s.cap};
-  G2J S;
-  if (codes[i] != 0) {
-    jac_set_inf(S);
-    rs.st_g2j(S, i);
+  if (b0 & 0x40) {
+    uint32_t acc = b0 & 0x3f;
+    for (uint32_t i = 1; i < nbytes; ++i) acc |= b[i];
+    if (acc) bad = 1;
+    else inf = 1;
     return;
   }
-  const uint64_t r = rlc_scalar(seed, i);
-  G1A pk;
-  s.ld_g1a(pk, i);
-  G1J P;
-  jac_mul_u64(P, pk, r);
-  G1A rp;
-  jac_to_aff(rp, P);  // r != 0 mod the group order, pk != O
-  Slab o{s.p + (size_t)S_RP * 12 * s.cap, s.cap};
-  o.st_g1a(rp, i);
-  Slab sg{s.p + (size_t)S_SIG * 12 * s.cap, s.cap};
-  G2A sig;
-  sg.ld_g2a(sig, i);
-  jac_mul_u64(S, sig, r);
-  rs.st_g2j(S, i);
+  if (!limbs_lt_p(x_hi)) bad = 1;
+  if (nbytes == 96 && !limbs_lt_p(x_lo)) bad = 1;
+  uint32_t z = 0;
+  for (int k = 0; k < 12; ++k) z |= x_hi[k] | (nbytes == 96 ? x_lo[k] : 0u);
+  xzero = z == 0;
 }
 
-__global__ __launch_bounds__(WG) void k_miller(uint32_t n, Slab s, const int32_t* __restrict__ codes) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  Fp12 f;
-  if (codes[i] == 0) {
-    Slab rp{s.p + (size_t)S_RP * 12 * s.cap, s.cap};
-    Slab hh{s.p + (size_t)S_H * 12 * s.cap, s.cap};
-    G1A p;
-    G2A h;
-    rp.ld_g1a(p, i);
-    hh.ld_g2a(h, i);
-    miller_loop(f, p, h);
-  } else {
-    fp12_one(f);
+struct VmDev {  // a program in device memory
+  const uint4* code;
+  uint32_t nphases;
+  const uint16_t* in;   // device copies of the slot maps
+  const uint16_t* out;
+};
+
+#define VM_SLICES 4  // 16-lane slices per 64-lane workgroup
+
+__device__ __forceinline__ void load_consts(uint32_t* cst, const uint32_t* __restrict__ g, uint32_t n) {
+  for (uint32_t k = threadIdx.x; k < n * 12; k += blockDim.x) cst[k] = g[k];
+}
+
+__device__ __forceinline__ void slot_flag(uint32_t* slots, uint32_t s, uint32_t f) {
+  uint4* d = reinterpret_cast<uint4*>(slots + s * 12);
+  d[0] = make_uint4(f, 0, 0, 0);
+  d[1] = make_uint4(0, 0, 0, 0);
+  d[2] = make_uint4(0, 0, 0, 0);
+}
+
+__device__ __forceinline__ void slot_put(uint32_t* slots, uint32_t s, const uint32_t* v) {
+  for (int k = 0; k < 12; ++k) slots[s * 12 + k] = v[k];
+}
+
+__device__ __forceinline__ uint32_t slot_flag_get(const uint32_t* slots, uint32_t s) { return slots[s * 12]; }
+
+// Per vote: VM "vote" program + reference-precedence code + the vote's (f, r sigma)
+// contribution. LDS: constants, then VM_SLICES x (VM_VOTE_NSLOTS slots).
+__global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
+                                                Slab s, uint64_t seed, int32_t* __restrict__ codes) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / VM_VOTE_W, lane = threadIdx.x % VM_VOTE_W;
+  uint32_t* slots = lds + VM_NCONST * 12 + slice * (VM_VOTE_NSLOTS * 12 + 4);
+  uint32_t* hdr = slots + VM_VOTE_NSLOTS * 12;  // [pflags, code]
+  const uint32_t i = blockIdx.x * VM_SLICES + slice;
+  const bool active = i < n;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active) {
+    if (lane == 0) {
+      uint32_t x[12], bad, inf, sort, xz;
+      parse_hdr(pks + (size_t)i * 48, 48, x, x, bad, inf, sort, xz);
+      slot_put(slots, VM_VOTE_IN[VM_VOTE_IN_PK_X], x);
+      slot_flag(slots, VM_VOTE_IN[VM_VOTE_IN_PK_SORT], sort);
+      hdr[0] = bad | inf << 1 | xz << 2;
+    }
   }
-  Slab fo{s.p + (size_t)S_F * 12 * s.cap, s.cap};
-  fo.st_f12(f, i);
-}
-
-// out[t] = prod_{k in chunk t} in[k]
-__global__ __launch_bounds__(WG) void k_reduce_f(uint32_t n, uint32_t chunk, Slab in, Slab out) {
-  const uint32_t t = blockIdx.x * WG + threadIdx.x;
-  const uint32_t lo = t * chunk;
-  if (lo >= n) return;
-  const uint32_t hi = lo + chunk < n ? lo + chunk : n;
-  Fp12 acc, x;
-  in.ld_f12(acc, lo);
-  for (uint32_t k = lo + 1; k < hi; ++k) {
-    in.ld_f12(x, k);
-    fp12_mul(acc, acc, x);
+  __syncthreads();
+  if (active) {
+    if (lane == 1) {
+      uint32_t x1[12], x0[12], bad, inf, sort, xz;
+      parse_hdr(sigs + (size_t)i * 96, 96, x1, x0, bad, inf, sort, xz);
+      slot_put(slots, VM_VOTE_IN[VM_VOTE_IN_SIG_X1], x1);
+      slot_put(slots, VM_VOTE_IN[VM_VOTE_IN_SIG_X0], x0);
+      slot_flag(slots, VM_VOTE_IN[VM_VOTE_IN_SIG_SORT], sort);
+      hdr[0] |= (bad | inf << 1 | xz << 2) << 8;
+    } else if (lane >= 2 && lane < 6) {
+      Fp u;
+      s.ld(u, S_U + (lane - 2), i);
+      slot_put(slots, VM_VOTE_IN[VM_VOTE_IN_U00 + (lane - 2)], u.v);
+    }
   }
-  out.st_f12(acc, t);
-}
-
-__global__ __launch_bounds__(WG) void k_reduce_s(uint32_t n, uint32_t chunk, Slab in, Slab out) {
-  const uint32_t t = blockIdx.x * WG + threadIdx.x;
-  const uint32_t lo = t * chunk;
-  if (lo >= n) return;
-  const uint32_t hi = lo + chunk < n ? lo + chunk : n;
-  G2J acc, x;
-  in.ld_g2j(acc, lo);
-  for (uint32_t k = lo + 1; k < hi; ++k) {
-    in.ld_g2j(x, k);
-    jac_add(acc, acc, x);
+  __syncthreads();
+  vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, i));
+  if (active && lane == 0) {
+    const uint32_t pf = hdr[0];
+    const uint32_t pk_bad = pf & 1, pk_inf = (pf >> 1) & 1, pk_xz = (pf >> 2) & 1;
+    const uint32_t sg_bad = (pf >> 8) & 1, sg_inf = (pf >> 9) & 1, sg_xz = (pf >> 10) & 1;
+    const uint32_t pk_ok = slot_flag_get(slots, VM_VOTE_OUT[VM_VOTE_OUT_PK_OK]);
+    const uint32_t pk_grp = slot_flag_get(slots, VM_VOTE_OUT[VM_VOTE_OUT_PK_GRP]);
+    const uint32_t sg_ok = slot_flag_get(slots, VM_VOTE_OUT[VM_VOTE_OUT_SIG_OK]);
+    const uint32_t sg_grp = slot_flag_get(slots, VM_VOTE_OUT[VM_VOTE_OUT_SIG_GRP]);
+    const uint32_t h_inf = slot_flag_get(slots, VM_VOTE_OUT[VM_VOTE_OUT_H_INF]);
+    // consensus.rs:397-416: pk parse (102) > sig parse (1..3) > [core_verify] sig group (3) >
+    // pk infinity (6) > pk group (3) > H(m) = O or sig = O (5) > pairing (batch)
+    int32_t c;
+    if (pk_bad || (!pk_inf && (!pk_ok || pk_xz))) c = OVH_ERR_PUBKEY;
+    else if (sg_bad) c = BLST_BAD_ENCODING;
+    else if (!sg_inf && !sg_ok) c = BLST_POINT_NOT_ON_CURVE;
+    else if (!sg_inf && (sg_xz || !sg_grp)) c = BLST_POINT_NOT_IN_GROUP;
+    else if (pk_inf) c = BLST_PK_IS_INFINITY;
+    else if (!pk_grp) c = BLST_POINT_NOT_IN_GROUP;
+    else if (h_inf || sg_inf) c = BLST_VERIFY_FAIL;
+    else c = 0;
+    codes[i] = c;
+    hdr[1] = (uint32_t)c;
   }
-  out.st_g2j(acc, t);
-}
-
-// Pack (F, S) of one shard into the 864-byte partial (216 words, AoS).
-__global__ __launch_bounds__(WG) void k_pack_partial(Slab f, Slab s, uint32_t* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  for (int j = 0; j < 12; ++j)
-    for (int k = 0; k < 12; ++k) out[j * 12 + k] = f.p[(size_t)(j * 12 + k) * f.cap];
-  for (int j = 0; j < 6; ++j)
-    for (int k = 0; k < 12; ++k) out[144 + j * 12 + k] = s.p[(size_t)(j * 12 + k) * s.cap];
-}
-
-// Combined check over k partials: prod F * Miller(-G1, sum S) -> FE == 1.
-__global__ __launch_bounds__(WG) void k_final(uint32_t k, const uint32_t* __restrict__ parts, int32_t* __restrict__ result) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  Fp12 F, x;
-  G2J S, y;
-  fp12_one(F);
-  jac_set_inf(S);
-  for (uint32_t q = 0; q < k; ++q) {
-    const uint32_t* p = parts + (size_t)q * 216;
-    Fp* c = &x.c0.c0.c0;
-    for (int j = 0; j < 12; ++j)
-      for (int l = 0; l < 12; ++l) c[j].v[l] = p[j * 12 + l];
-    Fp* d = &y.X.c0;
-    for (int j = 0; j < 6; ++j)
-      for (int l = 0; l < 12; ++l) d[j].v[l] = p[144 + j * 12 + l];
-    fp12_mul(F, F, x);
-    jac_add(S, S, y);
+  __syncthreads();
+  if (active) {
+    const bool ok = hdr[1] == 0;
+    // outputs 5.. : f (12), s (6), fallback (12) -> planes S_F, S_RS, S_FB
+    for (uint32_t k = lane; k < 30; k += VM_VOTE_W) {
+      Fp v;
+      const uint32_t src = VM_VOTE_OUT[VM_VOTE_OUT_F0 + k];
+      for (int q = 0; q < 12; ++q) v.v[q] = slots[src * 12 + q];
+      uint32_t plane;
+      if (k < 12) {
+        plane = S_F + k;
+        if (!ok) { if (k == 0) fp_one(v); else fp_zero(v); }
+      } else if (k < 18) {
+        plane = S_RS + (k - 12);
+        if (!ok) { if (k == 14) fp_one(v); else fp_zero(v); }  // O = (0 : 1 : 0)
+      } else {
+        plane = S_FB + (k - 18);
+      }
+      s.st(v, plane, i);
+    }
   }
-  G2A sa;
-  if (jac_to_aff(sa, S)) {
-    G1A ng1;
-    fp_load(ng1.x, G1X_M);
-    fp_load(ng1.y, G1NY_M);
-    Fp12 m;
-    miller_loop(m, ng1, sa);
-    fp12_mul(F, F, m);
-  }
-  final_exponentiation(F, F);
-  *result = fp12_is_one(F) ? 1 : 0;
 }
 
-__global__ __launch_bounds__(WG) void k_fallback(uint32_t n, Slab s, int32_t* __restrict__ codes) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n || codes[i] != 0) return;
-  G1A pk;
-  G2A sig, h;
-  s.ld_g1a(pk, i);
-  Slab sg{s.p + (size_t)S_SIG * 12 * s.cap, s.cap};
-  Slab hh{s.p + (size_t)S_H * 12 * s.cap, s.cap};
-  sg.ld_g2a(sig, i);
-  hh.ld_g2a(h, i);
-  codes[i] = pairing_check(pk, h, sig) ? 0 : BLST_VERIFY_FAIL;
+// Fold: out[t] = (prod F, sum S) over in[4t .. 4t+3] (missing -> identity).
+__global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
+                                                Slab inS, Slab out) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / VM_FOLD_W, lane = threadIdx.x % VM_FOLD_W;
+  uint32_t* slots = lds + VM_NCONST * 12 + slice * VM_FOLD_NSLOTS * 12;
+  const uint32_t t = blockIdx.x * VM_SLICES + slice;
+  const bool active = 4 * t < m;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active) {
+    for (uint32_t k = lane; k < 4 * PART_PLANES; k += VM_FOLD_W) {
+      const uint32_t q = k / PART_PLANES, j = k % PART_PLANES, e = 4 * t + q;
+      Fp v;
+      if (e < m) {
+        if (j < 12) inF.ld(v, j, e);
+        else inS.ld(v, j - 12, e);
+      } else if (j == 0 || j == 12 + 2) {
+        fp_one(v);
+      } else {
+        fp_zero(v);
+      }
+      slot_put(slots, VM_FOLD_IN[k], v.v);
+    }
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0);
+  if (active) {
+    for (uint32_t k = lane; k < PART_PLANES; k += VM_FOLD_W) {
+      Fp v;
+      const uint32_t src = VM_FOLD_OUT[k];
+      for (int q = 0; q < 12; ++q) v.v[q] = slots[src * 12 + q];
+      out.st(v, k, t);
+    }
+  }
+}
+
+// Final: prod F * Miller(-G1, sum S) over in[0..m-1] (m <= 4) -> FE == 1 -> *result.
+__global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
+                                                 Slab inS, int32_t* __restrict__ result) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  uint32_t* slots = lds + VM_NCONST * 12;
+  const uint32_t lane = threadIdx.x;
+  load_consts(cst, cst_g, VM_NCONST);
+  for (uint32_t k = lane; k < 4 * PART_PLANES; k += 64) {
+    const uint32_t q = k / PART_PLANES, j = k % PART_PLANES;
+    Fp v;
+    if (q < m) {
+      if (j < 12) inF.ld(v, j, q);
+      else inS.ld(v, j - 12, q);
+    } else if (j == 0 || j == 12 + 2) {
+      fp_one(v);
+    } else {
+      fp_zero(v);
+    }
+    slot_put(slots, VM_FINAL_IN[k], v.v);
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0);
+  if (lane == 0) *result = slot_flag_get(slots, VM_FINAL_OUT[0]) ? 1 : 0;
+}
+
+// Per-vote fallback: codes[i] (still 0) := e(pk, H) == e(G1, sigma) ? 0 : VERIFY_FAIL.
+__global__ __launch_bounds__(64) void k_vm_pairchk(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g, Slab s,
+                                                   int32_t* __restrict__ codes) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / VM_PAIRCHK_W, lane = threadIdx.x % VM_PAIRCHK_W;
+  uint32_t* slots = lds + VM_NCONST * 12 + slice * VM_PAIRCHK_NSLOTS * 12;
+  const uint32_t i = blockIdx.x * VM_SLICES + slice;
+  const bool active = i < n && codes[i] == 0;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active)
+    for (uint32_t k = lane; k < 12; k += VM_PAIRCHK_W) {
+      Fp v;
+      s.ld(v, S_FB + k, i);
+      slot_put(slots, VM_PAIRCHK_IN[k], v.v);
+    }
+  __syncthreads();
+  vm::run(prog.code, VM_PAIRCHK_NPHASES, VM_PAIRCHK_W, lane, active, slots, cst, 0);
+  if (active && lane == 0) codes[i] = slot_flag_get(slots, VM_PAIRCHK_OUT[0]) ? 0 : BLST_VERIFY_FAIL;
+}
+
+// AoS partials (216 words: F 144, S 72) -> planes
+__global__ __launch_bounds__(64) void k_unpack_partials(uint32_t k, const uint32_t* __restrict__ parts, Slab F, Slab S) {
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= k * PART_PLANES) return;
+  const uint32_t q = t / PART_PLANES, j = t % PART_PLANES;
+  Fp v;
+  for (int l = 0; l < 12; ++l) v.v[l] = parts[(size_t)q * 216 + j * 12 + l];
+  if (j < 12) F.st(v, j, q);
+  else S.st(v, j - 12, q);
+}
+
+// planes element 0 -> AoS partial
+__global__ __launch_bounds__(64) void k_pack_partial2(Slab F, Slab S, uint32_t* __restrict__ out) {
+  const uint32_t t = threadIdx.x;
+  if (t >= PART_PLANES) return;
+  Fp v;
+  if (t < 12) F.ld(v, t, 0);
+  else S.ld(v, t - 12, 0);
+  for (int l = 0; l < 12; ++l) out[t * 12 + l] = v.v[l];
 }
 
 // ---- single-call kernels (one lane) ----
@@ -511,14 +539,71 @@ struct ovh_ctx {
   uint32_t* partial = nullptr;   // 216 words
   int32_t* result = nullptr;     // device scalar
   uint32_t last_n = 0;
+  // Fp-VM programs + constant table in device memory
+  VmDev vm_vote{}, vm_fold{}, vm_final{}, vm_pairchk{};
+  uint32_t* vm_consts = nullptr;
+  std::vector<void*> vm_bufs;
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
   hipEvent_t ev0[OVH_NSTAGES] = {}, ev1[OVH_NSTAGES] = {};
   uint32_t ev_mask = 0;
 };
 
-static const char* const STAGE_NAMES[OVH_NSTAGES] = {
-    "parse_pk", "parse_sig", "codes", "hash_to_field", "sswu_iso", "h2c_finish",
-    "rlc_scalar", "miller", "reduce", "final", "fallback"};
+#define HIPCHK(x)                                  \
+  do {                                             \
+    if ((x) != hipSuccess) return OVH_ERR_DEVICE;  \
+  } while (0)
+
+static const char* const STAGE_NAMES[OVH_NSTAGES] = {"hash_to_field", "vote", "fold", "final", "fallback"};
+
+// LDS bytes of the VM kernels: constants + slices x slots (+ a 16-byte slice header for vote)
+static constexpr size_t LDS_VOTE = (size_t)VM_NCONST * 48 + VM_SLICES * ((size_t)VM_VOTE_NSLOTS * 48 + 16);
+static constexpr size_t LDS_FOLD = (size_t)VM_NCONST * 48 + VM_SLICES * (size_t)VM_FOLD_NSLOTS * 48;
+static constexpr size_t LDS_FINAL = (size_t)VM_NCONST * 48 + (size_t)VM_FINAL_NSLOTS * 48;
+static constexpr size_t LDS_PAIRCHK = (size_t)VM_NCONST * 48 + VM_SLICES * (size_t)VM_PAIRCHK_NSLOTS * 48;
+static_assert(VM_VOTE_W * VM_SLICES == 64 && VM_FOLD_W * VM_SLICES == 64 && VM_PAIRCHK_W * VM_SLICES == 64 &&
+                  VM_FINAL_W == 64, "VM slice widths");
+static_assert(LDS_VOTE <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
+
+static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphases, uint32_t W, const uint16_t* in,
+                     uint32_t nin, const uint16_t* out, uint32_t nout) {
+  const size_t words = (size_t)nphases * W * 4, pad = (size_t)W * 4;  // + one NOP phase
+  void *dc = nullptr, *di = nullptr, *dout = nullptr;
+  HIPCHK(hipMalloc(&dc, (words + pad) * 4));
+  c->vm_bufs.push_back(dc);
+  HIPCHK(hipMemcpy(dc, code, words * 4, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset((uint32_t*)dc + words, 0, pad * 4));
+  HIPCHK(hipMalloc(&di, nin * 2 + 2));
+  c->vm_bufs.push_back(di);
+  HIPCHK(hipMemcpy(di, in, nin * 2, hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&dout, nout * 2 + 2));
+  c->vm_bufs.push_back(dout);
+  HIPCHK(hipMemcpy(dout, out, nout * 2, hipMemcpyHostToDevice));
+  d.code = (const uint4*)dc;
+  d.nphases = nphases;
+  d.in = (const uint16_t*)di;
+  d.out = (const uint16_t*)dout;
+  return 0;
+}
+
+static int vm_init(ovh_ctx* c) {
+  HIPCHK(hipMalloc(&c->vm_consts, sizeof(VM_CONST_WORDS)));
+  HIPCHK(hipMemcpy(c->vm_consts, VM_CONST_WORDS, sizeof(VM_CONST_WORDS), hipMemcpyHostToDevice));
+  if (vm_upload(c, c->vm_vote, VM_VOTE_CODE, VM_VOTE_NPHASES, VM_VOTE_W, VM_VOTE_IN, VM_VOTE_NIN, VM_VOTE_OUT,
+                VM_VOTE_NOUT) ||
+      vm_upload(c, c->vm_fold, VM_FOLD_CODE, VM_FOLD_NPHASES, VM_FOLD_W, VM_FOLD_IN, VM_FOLD_NIN, VM_FOLD_OUT,
+                VM_FOLD_NOUT) ||
+      vm_upload(c, c->vm_final, VM_FINAL_CODE, VM_FINAL_NPHASES, VM_FINAL_W, VM_FINAL_IN, VM_FINAL_NIN,
+                VM_FINAL_OUT, VM_FINAL_NOUT) ||
+      vm_upload(c, c->vm_pairchk, VM_PAIRCHK_CODE, VM_PAIRCHK_NPHASES, VM_PAIRCHK_W, VM_PAIRCHK_IN,
+                VM_PAIRCHK_NIN, VM_PAIRCHK_OUT, VM_PAIRCHK_NOUT))
+    return OVH_ERR_DEVICE;
+  HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE));
+  HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FOLD));
+  HIPCHK(hipFuncSetAttribute((const void*)k_vm_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FINAL));
+  HIPCHK(hipFuncSetAttribute((const void*)k_vm_pairchk, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)LDS_PAIRCHK));
+  return 0;
+}
 
 // Stage bracket: events on the context's stream around the stage's kernels.
 struct StageScope {
@@ -535,10 +620,6 @@ struct StageScope {
   }
 };
 
-#define HIPCHK(x)                                  \
-  do {                                             \
-    if ((x) != hipSuccess) return OVH_ERR_DEVICE;  \
-  } while (0)
 
 static const uint8_t DEFAULT_DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_";
 
@@ -557,8 +638,8 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
   c->state = nullptr;
   c->red = nullptr;
   HIPCHK(hipMalloc(&c->state, (size_t)S_TOTAL * 12 * cap * 4));
-  c->red_cap = cap / 8 > 64 ? cap / 8 : 64;
-  HIPCHK(hipMalloc(&c->red, (size_t)2 * 18 * 12 * c->red_cap * 4));
+  c->red_cap = cap / 4 > 64 ? cap / 4 : 64;
+  HIPCHK(hipMalloc(&c->red, (size_t)2 * PART_PLANES * 12 * c->red_cap * 4));
   HIPCHK(hipMalloc(&c->st_pk, (size_t)cap * 4));
   HIPCHK(hipMalloc(&c->st_sig, (size_t)cap * 4));
   HIPCHK(hipMalloc(&c->codes, (size_t)cap * 4));
@@ -595,6 +676,10 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
     delete c;
     return nullptr;
   }
+  if (vm_init(c)) {
+    ovh_destroy(c);
+    return nullptr;
+  }
   if (flags & OVH_FLAG_PROFILE)
     for (int k = 0; k < OVH_NSTAGES; ++k)
       if (hipEventCreate(&c->ev0[k]) != hipSuccess || hipEventCreate(&c->ev1[k]) != hipSuccess) {
@@ -609,8 +694,9 @@ void ovh_destroy(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (void* p : {(void*)c->state, (void*)c->red, (void*)c->st_pk, (void*)c->st_sig, (void*)c->codes,
-                  (void*)c->in_buf, (void*)c->partial, (void*)c->result})
+                  (void*)c->in_buf, (void*)c->partial, (void*)c->result, (void*)c->vm_consts})
     if (p) (void)hipFree(p);
+  for (void* p : c->vm_bufs) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (int k = 0; k < OVH_NSTAGES; ++k) {
     if (c->ev0[k]) (void)hipEventDestroy(c->ev0[k]);
@@ -856,44 +942,42 @@ int ovh_verify_aggregated(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, co
 }
 
 // ---- batch ----
+// Per-vote stages + fold tree down to <= 4 partials (*outF / *outS planes, *out_m elements).
 static int batch_front(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
-                       uint64_t seed, int32_t* d_codes) {
+                       uint64_t seed, int32_t* d_codes, Slab* outF, Slab* outS, uint32_t* out_m) {
   Slab s{c->state, c->cap};
-  Slab sig{c->state + (size_t)S_SIG * 12 * c->cap, c->cap};
   hipStream_t st = c->stream;
   c->ev_mask = 0;
-  { StageScope p(c, ST_PARSE_PK); k_parse_pk<<<nblk(n), WG, 0, st>>>(n, d_pks, c->st_pk, s); }
-  { StageScope p(c, ST_PARSE_SIG); k_parse_sig<<<nblk(n), WG, 0, st>>>(n, d_sigs, c->st_sig, sig); }
-  { StageScope p(c, ST_CODES); k_codes<<<nblk(n), WG, 0, st>>>(n, c->st_pk, c->st_sig, d_codes); }
+  const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
   { StageScope p(c, ST_H2F); k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s); }
-  { StageScope p(c, ST_SSWU); k_sswu<<<nblk(2 * (size_t)n), WG, 0, st>>>(n, s); }
-  { StageScope p(c, ST_H2C_FIN); k_h2c_fin<<<nblk(n), WG, 0, st>>>(n, s, d_codes); }
-  { StageScope p(c, ST_SCALAR); k_scalar<<<nblk(n), WG, 0, st>>>(n, seed, s, d_codes); }
-  { StageScope p(c, ST_MILLER); k_miller<<<nblk(n), WG, 0, st>>>(n, s, d_codes); }
-  HIPCHK(hipGetLastError());
-  // reductions
-  const uint32_t chunk = 16;
-  Slab fin{c->state + (size_t)S_F * 12 * c->cap, c->cap};
-  Slab sin{c->state + (size_t)S_RS * 12 * c->cap, c->cap};
   {
-    StageScope p(c, ST_REDUCE);
-    uint32_t m = n;
-    int flip = 0;
-    while (m > 1) {
-      const uint32_t mo = (m + chunk - 1) / chunk;
-      uint32_t* base = c->red + (size_t)flip * 18 * 12 * c->red_cap;
-      Slab fo{base, c->red_cap}, so{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
-      k_reduce_f<<<nblk(mo), WG, 0, st>>>(m, chunk, fin, fo);
-      k_reduce_s<<<nblk(mo), WG, 0, st>>>(m, chunk, sin, so);
-      fin = fo;
-      sin = so;
+    StageScope p(c, ST_VOTE);
+    k_vm_vote<<<nwg, 64, LDS_VOTE, st>>>(n, c->vm_vote, c->vm_consts, d_pks, d_sigs, s, seed, d_codes);
+  }
+  HIPCHK(hipGetLastError());
+  // fold tree: level 0 reads the state planes (F at S_F, S at S_RS), later levels the
+  // ping-pong scratch (F planes 0..11, S planes 12..17)
+  Slab inF{c->state + (size_t)S_F * 12 * c->cap, c->cap}, inS{c->state + (size_t)S_RS * 12 * c->cap, c->cap};
+  uint32_t m = n;
+  int flip = 0;
+  {
+    StageScope p(c, ST_FOLD);
+    while (m > 4) {
+      const uint32_t mo = (m + 3) / 4;
+      uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
+      Slab o{base, c->red_cap};
+      k_vm_fold<<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, st>>>(m, c->vm_fold, c->vm_consts, inF, inS, o);
+      inF = o;
+      inS = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
       m = mo;
       flip ^= 1;
     }
-    k_pack_partial<<<1, WG, 0, st>>>(fin, sin, c->partial);
   }
   HIPCHK(hipGetLastError());
   c->last_n = n;
+  *outF = inF;
+  *outS = inS;
+  *out_m = m;
   return 0;
 }
 
@@ -903,19 +987,41 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) {
-    // neutral partial: F = 1, S = O
+    // neutral partial: F = 1, S = O = (0 : 1 : 0)
     std::vector<uint32_t> p(216, 0);
     for (int k = 0; k < 12; ++k) p[k] = ONE_M[k];
-    for (int k = 0; k < 12; ++k) p[144 + k] = ONE_M[k];       // X = 1
-    for (int k = 0; k < 12; ++k) p[144 + 24 + k] = ONE_M[k];  // Y = 1 (Z = 0)
+    for (int k = 0; k < 12; ++k) p[144 + 24 + k] = ONE_M[k];  // Y.c0 = 1
     HIPCHK(hipMemcpyAsync(d_partial, p.data(), 864, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
   }
   if (ensure_cap(c, n)) return OVH_ERR_DEVICE;
-  int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes);
+  Slab F, S;
+  uint32_t m;
+  int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m);
   if (e) return e;
-  HIPCHK(hipMemcpyAsync(d_partial, c->partial, 864, hipMemcpyDeviceToDevice, c->stream));
+  if (m > 1) {  // fold the last <= 4 into one partial
+    uint32_t* base = c->red + (size_t)(F.p == c->red ? 1 : 0) * PART_PLANES * 12 * c->red_cap;
+    Slab o{base, c->red_cap};
+    k_vm_fold<<<1, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o);
+    F = o;
+  }
+  // pack element 0 (F planes, S planes) into the AoS partial
+  k_pack_partial2<<<1, 64, 0, c->stream>>>(F, m > 1 ? Slab{F.p + (size_t)12 * 12 * F.cap, F.cap} : S,
+                                           (uint32_t*)d_partial);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// Combined check on <= 4 partials given as planes (fold further if needed by the caller).
+static int final_check(ovh_ctx* c, Slab F, Slab S, uint32_t m, int32_t* r_host) {
+  {
+    StageScope p(c, ST_FINAL);
+    k_vm_final<<<1, 64, LDS_FINAL, c->stream>>>(m, c->vm_final, c->vm_consts, F, S, c->result);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(r_host, c->result, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
@@ -924,14 +1030,28 @@ int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials)
   if (!c || !d_partials || k == 0 || k > 4096) return -OVH_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return -OVH_ERR_DEVICE;
-  {
-    StageScope p(c, ST_FINAL);
-    k_final<<<1, WG, 0, c->stream>>>((uint32_t)k, (const uint32_t*)d_partials, c->result);
+  if (ensure_cap(c, k * 4 > 256 ? k * 4 : 256)) return -OVH_ERR_DEVICE;
+  // AoS partials -> planes in the state slab (F at S_F, S at S_RS), then fold to <= 4
+  Slab s{c->state, c->cap};
+  Slab F{c->state + (size_t)S_F * 12 * c->cap, c->cap}, S{c->state + (size_t)S_RS * 12 * c->cap, c->cap};
+  k_unpack_partials<<<(uint32_t)((k * PART_PLANES + 63) / 64), 64, 0, c->stream>>>((uint32_t)k,
+                                                                                   (const uint32_t*)d_partials, F, S);
+  uint32_t m = (uint32_t)k;
+  int flip = 0;
+  while (m > 4) {
+    const uint32_t mo = (m + 3) / 4;
+    uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
+    Slab o{base, c->red_cap};
+    k_vm_fold<<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o);
+    F = o;
+    S = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
+    m = mo;
+    flip ^= 1;
   }
+  (void)s;
   if (hipGetLastError() != hipSuccess) return -OVH_ERR_DEVICE;
   int32_t r = -1;
-  if (hipMemcpyAsync(&r, c->result, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return -OVH_ERR_DEVICE;
-  if (hipStreamSynchronize(c->stream) != hipSuccess) return -OVH_ERR_DEVICE;
+  if (final_check(c, F, S, m, &r)) return -OVH_ERR_DEVICE;
   return r;
 }
 
@@ -944,7 +1064,8 @@ int ovh_batch_fallback_device(ovh_ctx* c, size_t n, int32_t* d_codes) {
   Slab s{c->state, c->cap};
   {
     StageScope p(c, ST_FALLBACK);
-    k_fallback<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, s, d_codes);
+    k_vm_pairchk<<<(uint32_t)((n + VM_SLICES - 1) / VM_SLICES), 64, LDS_PAIRCHK, c->stream>>>(
+        (uint32_t)n, c->vm_pairchk, c->vm_consts, s, d_codes);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -958,20 +1079,19 @@ int ovh_verify_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const u
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   if (ensure_cap(c, n)) return OVH_ERR_DEVICE;
-  int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes);
+  Slab F, S;
+  uint32_t m;
+  int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m);
   if (e) return e;
-  {
-    StageScope p(c, ST_FINAL);
-    k_final<<<1, WG, 0, c->stream>>>(1, c->partial, c->result);
-  }
-  HIPCHK(hipGetLastError());
   int32_t r = -1;
-  HIPCHK(hipMemcpyAsync(&r, c->result, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (final_check(c, F, S, m, &r)) return OVH_ERR_DEVICE;
   if (r != 1) {
     Slab s{c->state, c->cap};
-    StageScope p(c, ST_FALLBACK);
-    k_fallback<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, s, d_codes);
+    {
+      StageScope p(c, ST_FALLBACK);
+      k_vm_pairchk<<<(uint32_t)((n + VM_SLICES - 1) / VM_SLICES), 64, LDS_PAIRCHK, c->stream>>>(
+          (uint32_t)n, c->vm_pairchk, c->vm_consts, s, d_codes);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
   }

@@ -44,7 +44,7 @@ typedef struct ovh_ctx ovh_ctx;
 
 /* Batch stages (ovh_stage_name gives the label). Each stage is one or more kernels enqueued
  * back to back on ovh_stream. */
-#define OVH_NSTAGES 11
+#define OVH_NSTAGES 5
 
 /* Create a context on HIP device `device` with hash-to-curve domain separation tag `dst`
  * (NULL -> "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_", the believed ophelia-blst DST).
@@ -92,8 +92,9 @@ int ovh_verify_batch_device(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const
                             const uint8_t* d_pks, uint64_t seed, int32_t* d_codes);
 
 /* Multi-GPU split of ovh_verify_batch_device: per-shard partial = {Fp12 product of the
- * shard's Miller outputs (576 B), Jacobian G2 sum of r_i sigma_i (288 B)} = 864 bytes,
- * written to d_partial (device memory). Per-vote parse/subgroup codes go to d_codes. */
+ * shard's Miller outputs (576 B), projective G2 sum of r_i sigma_i (288 B)} = 864 bytes,
+ * written to d_partial (device memory). Per-vote parse/subgroup codes go to d_codes.
+ * The G2 sum is in homogeneous projective coordinates (X : Y : Z), O = (0 : 1 : 0). */
 #define OVH_PARTIAL_BYTES 864
 int ovh_batch_partial_device(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
                              const uint8_t* d_pks, uint64_t seed, int32_t* d_codes, uint8_t* d_partial);

@@ -1,0 +1,142 @@
+"""The Fp-VM programs of the batch verifier (built from alg.py), with their input / output
+layouts. Input and output names are listed in the order the HIP side addresses them.
+
+  vote     one vote of ovh_verify_batch: pk decompress + G1 subgroup
+           check, sig decompress + G2 subgroup check, hash_to_G2 from (u0, u1), the RLC
+           scalar products r pk (affine) and r sigma (projective), f = Miller(r pk, H).
+  fold     4 partials (F_i in Fp12, S_i projective G2) -> (prod F_i, sum S_i)
+  final    up to 4 partials -> prod F * Miller(-G1, sum S) -> final exponentiation == 1
+  pairchk  per-vote fallback: e(pk, H) == e(G1, sigma)
+"""
+from __future__ import annotations
+
+from alg import G1X, G1Y, Alg
+from ir import P, Prog
+
+R_MONT = pow(2, 384, P)
+
+
+def f12_names(prefix):
+    return ["%s%d" % (prefix, j) for j in range(12)]
+
+
+def g2p_names(prefix):
+    return ["%s%d" % (prefix, j) for j in range(6)]
+
+
+def flat12(f):
+    return [c for f6 in f for f2 in f6 for c in f2]
+
+
+def unflat12(v):
+    return ((tuple(v[0:2]), tuple(v[2:4]), tuple(v[4:6])), (tuple(v[6:8]), tuple(v[8:10]), tuple(v[10:12])))
+
+
+def flat_g2p(pt):
+    return [c for f2 in pt for c in f2]
+
+
+def unflat_g2p(v):
+    return (tuple(v[0:2]), tuple(v[2:4]), tuple(v[4:6]))
+
+
+VOTE_IN = ["pk_x", "pk_sort", "sig_x0", "sig_x1", "sig_sort", "u00", "u01", "u10", "u11"]
+VOTE_OUT = (["pk_ok", "pk_grp", "sig_ok", "sig_grp", "h_inf"] + f12_names("f") + g2p_names("s")
+            + ["pkx", "pky", "sx0", "sx1", "sy0", "sy1"] + g2p_names("h"))
+
+
+def build_vote():
+    p = Prog("vote")
+    a = Alg(p)
+    R = p.const(R_MONT)
+    pkx = p.input("pk_x") * R
+    sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
+    u0 = (p.input("u00"), p.input("u01"))
+    u1 = (p.input("u10"), p.input("u11"))
+    pk_ok, (px, py) = a.g1_decompress(pkx, p.input("pk_sort"))
+    Pp = (px, py, p.one)
+    pk_grp, _ = a.g1_in_group(Pp)
+    sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
+    Qs = (qx, qy, (p.one, p.zero))
+    sig_grp = a.g2_in_group(Qs)
+    H = a.hash_to_g2(u0, u1)
+    h_inf = a.f2_is_zero(H[2])
+    rP = a.to_affine("fp", a.pt_mul_rbits("fp", Pp, 64))
+    rS = a.pt_mul_rbits("f2", Qs, 64)
+    f = a.miller_loop(rP, H)
+    outs = [pk_ok, pk_grp, sig_ok, sig_grp, h_inf] + flat12(f) + flat_g2p(rS) + [px, py, qx[0], qx[1], qy[0], qy[1]] \
+        + flat_g2p(H)
+    for name, v in zip(VOTE_OUT, outs):
+        p.output(name, v)
+    return p
+
+
+FOLD_K = 4
+FOLD_IN = [n for k in range(FOLD_K) for n in f12_names("F%d_" % k) + g2p_names("S%d_" % k)]
+FOLD_OUT = f12_names("F") + g2p_names("S")
+
+
+def build_fold():
+    p = Prog("fold")
+    a = Alg(p)
+    Fs, Ss = [], []
+    for k in range(FOLD_K):
+        Fs.append(unflat12([p.input(n) for n in f12_names("F%d_" % k)]))
+        Ss.append(unflat_g2p([p.input(n) for n in g2p_names("S%d_" % k)]))
+    F01 = a.f12_mul(Fs[0], Fs[1])
+    F23 = a.f12_mul(Fs[2], Fs[3])
+    S01 = a.pt_add("f2", Ss[0], Ss[1])
+    S23 = a.pt_add("f2", Ss[2], Ss[3])
+    F = a.f12_mul(F01, F23)
+    S = a.pt_add("f2", S01, S23)
+    for name, v in zip(FOLD_OUT, flat12(F) + flat_g2p(S)):
+        p.output(name, v)
+    return p
+
+
+FINAL_IN = FOLD_IN
+FINAL_OUT = ["ok"]
+
+
+def build_final():
+    p = Prog("final")
+    a = Alg(p)
+    Fs, Ss = [], []
+    for k in range(FOLD_K):
+        Fs.append(unflat12([p.input(n) for n in f12_names("F%d_" % k)]))
+        Ss.append(unflat_g2p([p.input(n) for n in g2p_names("S%d_" % k)]))
+    F = a.f12_mul(a.f12_mul(Fs[0], Fs[1]), a.f12_mul(Fs[2], Fs[3]))
+    S = a.pt_add("f2", a.pt_add("f2", Ss[0], Ss[1]), a.pt_add("f2", Ss[2], Ss[3]))
+    s_inf = a.f2_is_zero(S[2])
+    ng1 = (p.const(G1X), p.const(-G1Y))
+    m = a.miller_loop(ng1, S)
+    one = a.f12_one()
+    m = unflat12([p.sel(s_inf, x, y) for x, y in zip(flat12(m), flat12(one))])
+    fe = a.final_exp(a.f12_mul(F, m))
+    p.output("ok", a.f12_eq_one(fe))
+    return p
+
+
+PAIRCHK_IN = ["pkx", "pky", "sx0", "sx1", "sy0", "sy1"] + g2p_names("h")
+PAIRCHK_OUT = ["ok"]
+
+
+def build_pairchk():
+    p = Prog("pairchk")
+    a = Alg(p)
+    pk = (p.input("pkx"), p.input("pky"))
+    sig = ((p.input("sx0"), p.input("sx1")), (p.input("sy0"), p.input("sy1")), (p.one, p.zero))
+    H = unflat_g2p([p.input(n) for n in g2p_names("h")])
+    f1 = a.miller_loop(pk, H)
+    ng1 = (p.const(G1X), p.const(-G1Y))
+    f2 = a.miller_loop(ng1, sig)
+    p.output("ok", a.f12_eq_one(a.final_exp(a.f12_mul(f1, f2))))
+    return p
+
+
+PROGRAMS = {
+    "vote": (build_vote, VOTE_IN, VOTE_OUT),
+    "fold": (build_fold, FOLD_IN, FOLD_OUT),
+    "final": (build_final, FINAL_IN, FINAL_OUT),
+    "pairchk": (build_pairchk, PAIRCHK_IN, PAIRCHK_OUT),
+}

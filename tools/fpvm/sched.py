@@ -1,0 +1,281 @@
+"""Schedule a traced Fp-VM program (ir.Prog) onto W lanes, allocate LDS slots, encode the
+per-lane instruction stream, and re-execute the encoded stream slot by slot (simulate) to
+prove scheduling + allocation preserve the program's values.
+
+Round semantics (the interpreter, consensus_overlord_amd/csrc/fpvm.hpp): in round t every lane
+of a slice reads its operands from LDS slots / the constant table, computes one op and writes
+one slot; results are visible from round t + 1. A slot whose value was last read in round t can
+be rewritten from round t + 1 on.
+
+Instruction (4 x uint32 per lane per round):
+  w0 = opcode | sb << 5 | sy << 6 | sd << 7 | dst << 8 (11 bits) | imm << 20 (6 bits)
+  w1 = A | B << 16,  w2 = C | D << 16,  w3 = 0
+  operand: slot index (< CONST_BASE), CONST_BASE + k (constant table entry k), ABSENT (zero)
+  signs: 0 = +, 1 = -.
+"""
+from __future__ import annotations
+
+import heapq
+from collections import defaultdict
+
+from ir import HALF_P, HEAVY, P
+
+OPC = {"nop": 0, "muls": 1, "sgn0": 2, "lex": 3, "lin": 4, "sel": 5, "eq": 6, "and": 7, "or": 8, "xor": 9,
+       "rbit": 10}
+CONST_BASE = 0x800
+ABSENT = 0xFFFF
+R_MONT = pow(2, 384, P)
+
+
+class ConstTable:
+    """Constants shared by every program: (value, raw) -> index. raw constants are stored as
+    plain limbs; the others in Montgomery form (value * 2^384 mod p)."""
+
+    def __init__(self):
+        self.index = {}
+        self.entries = []
+
+    def ref(self, value, raw):
+        key = (value, bool(raw))
+        if key not in self.index:
+            self.index[key] = len(self.entries)
+            self.entries.append(key)
+        return CONST_BASE + self.index[key]
+
+    def words(self):
+        out = []
+        for value, raw in self.entries:
+            v = value if raw else value * R_MONT % P
+            out.append([(v >> (32 * k)) & 0xFFFFFFFF for k in range(12)])
+        return out
+
+
+class Scheduled:
+    def __init__(self, prog, W, rounds, slot_of, nslots, consts):
+        self.prog = prog
+        self.W = W
+        self.rounds = rounds          # list of list of op ids (len <= W)
+        self.slot_of = slot_of        # value id -> slot
+        self.nslots = nslots
+        self.consts = consts
+
+    @property
+    def nrounds(self):
+        return len(self.rounds)
+
+    def stats(self):
+        heavy_rounds = sum(1 for k in self.kinds if k == "H")
+        nheavy = sum(1 for r in self.rounds for i in r if self.prog.ops[i].kind in HEAVY)
+        nlight = sum(1 for r in self.rounds for i in r if self.prog.ops[i].kind not in HEAVY)
+        return {"phases": self.nrounds, "heavy_phases": heavy_rounds, "light_phases": self.nrounds - heavy_rounds,
+                "heavy_ops": nheavy, "light_ops": nlight, "slots": self.nslots, "W": self.W,
+                "lane_util_heavy": round(nheavy / max(1, heavy_rounds * self.W), 3),
+                "cost_est": heavy_rounds * 900 + (self.nrounds - heavy_rounds) * 150}
+
+
+def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1, mixed=True):
+    ops = prog.ops
+    live = prog.live_ops()
+    liveset = set(live)
+    pre = {i for i in live if ops[i].kind in ("in", "const")}
+    work = [i for i in live if i not in pre]
+    preds = {}
+    succs = defaultdict(list)
+    for i in work:
+        ps = {s for s in ops[i].srcs if s is not None and s not in pre}
+        preds[i] = ps
+        for s in ps:
+            succs[s].append(i)
+    prio = {}
+    for i in reversed(work):
+        c = heavy_w if ops[i].kind in HEAVY else light_w
+        prio[i] = c + max((prio[s] for s in succs[i]), default=0)
+    indeg = {i: len(preds[i]) for i in work}
+    hq, lq = [], []
+
+    def push(i):
+        heapq.heappush(hq if ops[i].kind in HEAVY else lq, (-prio[i], i))
+    for i in work:
+        if indeg[i] == 0:
+            push(i)
+    # Phases: a heavy phase (one Montgomery product per lane) is followed by up to
+    # `max_light` light phases while light ops are ready; results of a phase are visible to
+    # the next phase.
+    rounds = []
+    kinds = []
+    done = 0
+    while done < len(work):
+        top_h = -hq[0][0] if hq else -1
+        top_l = -lq[0][0] if lq else -1
+        cur = []
+        if top_l > top_h:
+            # the most critical ready op is light: a cheap light-only phase
+            kind = "L"
+            while lq and len(cur) < W:
+                cur.append(heapq.heappop(lq)[1])
+        else:
+            # heavy phase; idle lanes take light ops (divergent but cheap)
+            kind = "H"
+            while hq and len(cur) < W:
+                cur.append(heapq.heappop(hq)[1])
+            if mixed:
+                while lq and len(cur) < W:
+                    cur.append(heapq.heappop(lq)[1])
+        rounds.append(cur)
+        kinds.append(kind)
+        done += len(cur)
+        for i in cur:
+            for s in succs[i]:
+                indeg[s] -= 1
+                if indeg[s] == 0:
+                    push(s)
+    # ---- slot allocation
+    def_round = {i: -1 for i in pre if ops[i].kind == "in"}
+    for t, r in enumerate(rounds):
+        for i in r:
+            def_round[i] = t
+    last_use = defaultdict(lambda: -1)
+    for t, r in enumerate(rounds):
+        for i in r:
+            for s in ops[i].srcs:
+                if s is not None and ops[s].kind != "const":
+                    last_use[s] = max(last_use[s], t)
+    end = len(rounds)
+    for v in prog.outputs.values():
+        last_use[v] = end
+    slot_of = {}
+    free = []
+    nslots = 0
+    frees_at = defaultdict(list)   # round -> slots that become free at that round
+
+    def alloc(v):
+        nonlocal nslots
+        if free:
+            s = heapq.heappop(free)
+        else:
+            s = nslots
+            nslots += 1
+        slot_of[v] = s
+        lu = last_use[v]
+        if lu < 0:   # never read (dead write): free right after
+            lu = def_round[v]
+        frees_at[lu + 1].append(s)
+    for name in sorted(prog.inputs):
+        v = prog.inputs[name]
+        if v in liveset:
+            alloc(v)
+    for t, r in enumerate(rounds):
+        for s in frees_at.pop(t, []):
+            heapq.heappush(free, s)
+        for i in r:
+            alloc(i)
+    if max_slots is not None and nslots > max_slots:
+        raise RuntimeError("%s: %d slots > %d" % (prog.name, nslots, max_slots))
+    for i in pre:
+        if ops[i].kind == "const":
+            consts.ref(ops[i].imm, ops[i].name == "raw")
+    sc = Scheduled(prog, W, rounds, slot_of, nslots, consts)
+    sc.kinds = kinds
+    return sc
+
+
+def _operand(sc, v):
+    if v is None:
+        return ABSENT
+    op = sc.prog.ops[v]
+    if op.kind == "const":
+        return sc.consts.ref(op.imm, op.name == "raw")
+    return sc.slot_of[v]
+
+
+def encode(sc):
+    """-> list of uint32 words, nrounds * W * 4."""
+    words = []
+    ops = sc.prog.ops
+    for r in sc.rounds:
+        lanes = list(r) + [None] * (sc.W - len(r))
+        for i in lanes:
+            if i is None:
+                words += [0, 0, 0, 0]
+                continue
+            op = ops[i]
+            k = op.kind
+            s = list(op.srcs) + [None] * (4 - len(op.srcs))
+            sb = sy = sd = 0
+            if k in ("muls", "lin", "eq"):
+                sb = 1 if op.signs[0] < 0 else 0
+                sy = 1 if op.signs[1] < 0 else 0
+                sd = 1 if op.signs[2] < 0 else 0
+                A, B, C, D = s[0], s[1], s[2], s[3]
+            elif k in ("sgn0", "lex"):
+                A, B, C, D = s[0], None, None, None
+            elif k == "sel":           # A = flag, B = x, C = y
+                A, B, C, D = s[0], s[1], s[2], None
+            elif k in ("and", "or", "xor"):
+                A, B, C, D = s[0], None, s[1], None
+            elif k == "rbit":
+                A = B = C = D = None
+            else:
+                raise ValueError(k)
+            w0 = OPC[k] | sb << 5 | sy << 6 | sd << 7 | sc.slot_of[i] << 8 | (op.imm & 63) << 20
+            if k in ("sgn0", "lex"):
+                cref = sc.consts.ref(1, True)   # plain 1: from-Montgomery product
+                w2c = cref
+            else:
+                w2c = _operand(sc, C)
+            words += [w0, _operand(sc, A) | _operand(sc, B) << 16, w2c | _operand(sc, D) << 16, 0]
+    return words
+
+
+def simulate(sc, words, inputs: dict, scalar: int = 0):
+    """Execute the encoded stream on canonical values; returns {output name: value}."""
+    const_vals = sc.consts.entries
+    slots = [0] * sc.nslots
+    for name, v in sc.prog.inputs.items():
+        if v in sc.slot_of:
+            slots[sc.slot_of[v]] = inputs[name] % P
+
+    def get(ref):
+        if ref == ABSENT:
+            return 0
+        if ref >= CONST_BASE:
+            val, raw = const_vals[ref - CONST_BASE]
+            return val
+        return slots[ref]
+    W = sc.W
+    for t in range(sc.nrounds):
+        results = []
+        for lane in range(W):
+            w0, w1, w2, _ = words[(t * W + lane) * 4:(t * W + lane) * 4 + 4]
+            opc = w0 & 31
+            if opc == 0:
+                continue
+            sb, sy, sd = (w0 >> 5) & 1, (w0 >> 6) & 1, (w0 >> 7) & 1
+            dst = (w0 >> 8) & 0x7FF
+            imm = (w0 >> 20) & 63
+            A, B, C, D = get(w1 & 0xFFFF), get(w1 >> 16), get(w2 & 0xFFFF), get(w2 >> 16)
+            if opc == 5:
+                z = C if A else B
+            elif opc in (7, 8, 9):
+                z = (A & C) if opc == 7 else (A | C) if opc == 8 else (A ^ C)
+            elif opc == 10:
+                z = (scalar >> imm) & 1
+            else:
+                x = (A - B if sb else A + B) % P
+                y = (C - D if sd else C + D) % P
+                if opc == 1:
+                    z = x * y % P
+                elif opc == 2:
+                    z = x & 1           # (x * plain1) = canonical x
+                elif opc == 3:
+                    z = 1 if x > HALF_P else 0
+                elif opc == 4:
+                    z = (x - y if sy else x + y) % P
+                elif opc == 6:
+                    z = 1 if x == y else 0
+                else:
+                    raise ValueError(opc)
+            results.append((dst, z))
+        for dst, z in results:
+            slots[dst] = z
+    return {name: slots[sc.slot_of[v]] for name, v in sc.prog.outputs.items()}
