@@ -14,7 +14,15 @@ namespace vm {
 
 enum : uint32_t {
   OP_NOP = 0, OP_MULS = 1, OP_SGN0 = 2, OP_LEX = 3, OP_LIN = 4, OP_SEL = 5, OP_EQ = 6,
-  OP_AND = 7, OP_OR = 8, OP_XOR = 9, OP_RBIT = 10,
+  OP_AND = 7, OP_OR = 8, OP_XOR = 9, OP_RBIT = 10, OP_ST = 11, OP_SELB = 12,
+};
+
+// Where `st` ops write: plane `imm` of unit `unit` in a structure-of-arrays slab (limb k of
+// plane j at base[(j * 12 + k) * cap + unit]).
+struct Out {
+  uint32_t* base;
+  uint32_t cap;
+  uint32_t unit;
 };
 constexpr uint32_t CONST_BASE = 0x800;
 constexpr uint32_t ABSENT = 0xFFFF;
@@ -56,13 +64,22 @@ __device__ __forceinline__ void combine(Fp& x, const uint32_t* slots, const uint
 
 // One op of one lane. `in` = (w0, A|B<<16, C|D<<16, 0).
 __device__ __forceinline__ void exec(const uint4 in, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
-                                     uint64_t scalar) {
+                                     uint64_t scalar, const Out& out) {
   const uint32_t op = in.x & 31;
   if (op == OP_NOP) return;
   const uint32_t dst = (in.x >> 8) & 0x7FF;
   const uint32_t ra = in.y & 0xFFFF, rb = in.y >> 16, rc = in.z & 0xFFFF, rd = in.z >> 16;
   Fp z;
-  if (op == OP_RBIT) {
+  if (op == OP_ST) {
+    ld_slot(z, slots, cst, ra);
+    uint32_t* b = out.base + (size_t)((in.x >> 20) & 63) * 12 * out.cap + out.unit;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) b[(size_t)k * out.cap] = z.v[k];
+    return;
+  }
+  if (op == OP_SELB) {
+    ld_slot(z, slots, cst, ((scalar >> ((in.x >> 20) & 63)) & 1) ? rc : rb);
+  } else if (op == OP_RBIT) {
     set_flag(z, (uint32_t)(scalar >> ((in.x >> 20) & 63)) & 1u);
   } else if (op == OP_SEL) {
     Fp f;
@@ -95,13 +112,13 @@ __device__ __forceinline__ void exec(const uint4 in, uint32_t* __restrict__ slot
 // phase barrier is a workgroup barrier); lanes of inactive slices pass active = false.
 __device__ __forceinline__ void run(const uint4* __restrict__ code, uint32_t nphases, uint32_t W, uint32_t lane,
                                     bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
-                                    uint64_t scalar) {
+                                    uint64_t scalar, const Out& out) {
   uint4 nxt = code[lane];
 #pragma unroll 1
   for (uint32_t ph = 0; ph < nphases; ++ph) {
     const uint4 cur = nxt;
     nxt = code[(size_t)(ph + 1) * W + lane];  // code carries one trailing NOP phase
-    if (active) exec(cur, slots, cst, scalar);
+    if (active) exec(cur, slots, cst, scalar, out);
     __syncthreads();
   }
 }

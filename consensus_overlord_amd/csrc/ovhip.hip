@@ -88,11 +88,11 @@ struct Slab {
 
 // Fp planes of the per-vote state slab.
 enum : uint32_t {
-  S_U = 0,      // 4 planes: u0, u1 (hash_to_field, Montgomery)
-  S_FB = 4,     // 12 planes: pk affine (2), sig affine (4), H projective (6) -- fallback inputs
-  S_RS = 16,    // 6 planes: r * sig (projective)
-  S_F = 22,     // 12 planes: f = Miller(r pk, H)
-  S_TOTAL = 34,
+  S_U = VM_S_U,       // 4 planes: u0, u1 (hash_to_field, Montgomery)
+  S_FB = VM_S_FB,     // 12 planes: pk affine (2), sig affine (4), H projective (6) -- fallback inputs
+  S_RS = VM_S_RS,     // 6 planes: r * sig (projective)
+  S_F = VM_S_F,       // 12 planes: f = Miller(r pk, H)
+  S_TOTAL = VM_S_TOTAL,
 };
 // partial = (F: 12 planes, S: 6 planes)
 constexpr uint32_t PART_PLANES = 18;
@@ -219,7 +219,8 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, const ui
     }
   }
   __syncthreads();
-  vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, i));
+  vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, i),
+          vm::Out{s.p, s.cap, i});
   if (active && lane == 0) {
     const uint32_t pf = hdr[0];
     const uint32_t pk_bad = pf & 1, pk_inf = (pf >> 1) & 1, pk_xz = (pf >> 2) & 1;
@@ -241,34 +242,13 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, const ui
     else if (h_inf || sg_inf) c = BLST_VERIFY_FAIL;
     else c = 0;
     codes[i] = c;
-    hdr[1] = (uint32_t)c;
-  }
-  __syncthreads();
-  if (active) {
-    const bool ok = hdr[1] == 0;
-    // outputs 5.. : f (12), s (6), fallback (12) -> planes S_F, S_RS, S_FB
-    for (uint32_t k = lane; k < 30; k += VM_VOTE_W) {
-      Fp v;
-      const uint32_t src = VM_VOTE_OUT[VM_VOTE_OUT_F0 + k];
-      for (int q = 0; q < 12; ++q) v.v[q] = slots[src * 12 + q];
-      uint32_t plane;
-      if (k < 12) {
-        plane = S_F + k;
-        if (!ok) { if (k == 0) fp_one(v); else fp_zero(v); }
-      } else if (k < 18) {
-        plane = S_RS + (k - 12);
-        if (!ok) { if (k == 14) fp_one(v); else fp_zero(v); }  // O = (0 : 1 : 0)
-      } else {
-        plane = S_FB + (k - 18);
-      }
-      s.st(v, plane, i);
-    }
   }
 }
 
 // Fold: out[t] = (prod F, sum S) over in[4t .. 4t+3] (missing -> identity).
+// Level 0 (codes != nullptr) takes the identity for every vote whose code is not 0.
 __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
-                                                Slab inS, Slab out) {
+                                                Slab inS, Slab out, const int32_t* __restrict__ codes) {
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -281,7 +261,7 @@ __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const ui
     for (uint32_t k = lane; k < 4 * PART_PLANES; k += VM_FOLD_W) {
       const uint32_t q = k / PART_PLANES, j = k % PART_PLANES, e = 4 * t + q;
       Fp v;
-      if (e < m) {
+      if (e < m && (!codes || codes[e] == 0)) {
         if (j < 12) inF.ld(v, j, e);
         else inS.ld(v, j - 12, e);
       } else if (j == 0 || j == 12 + 2) {
@@ -293,7 +273,7 @@ __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const ui
     }
   }
   __syncthreads();
-  vm::run(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0);
+  vm::run(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
   if (active) {
     for (uint32_t k = lane; k < PART_PLANES; k += VM_FOLD_W) {
       Fp v;
@@ -327,7 +307,7 @@ __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const u
     slot_put(slots, VM_FINAL_IN[k], v.v);
   }
   __syncthreads();
-  vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0);
+  vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
   if (lane == 0) *result = slot_flag_get(slots, VM_FINAL_OUT[0]) ? 1 : 0;
 }
 
@@ -349,7 +329,7 @@ __global__ __launch_bounds__(64) void k_vm_pairchk(uint32_t n, VmDev prog, const
       slot_put(slots, VM_PAIRCHK_IN[k], v.v);
     }
   __syncthreads();
-  vm::run(prog.code, VM_PAIRCHK_NPHASES, VM_PAIRCHK_W, lane, active, slots, cst, 0);
+  vm::run(prog.code, VM_PAIRCHK_NPHASES, VM_PAIRCHK_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
   if (active && lane == 0) codes[i] = slot_flag_get(slots, VM_PAIRCHK_OUT[0]) ? 0 : BLST_VERIFY_FAIL;
 }
 
@@ -962,16 +942,18 @@ static int batch_front(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint
   int flip = 0;
   {
     StageScope p(c, ST_FOLD);
-    while (m > 4) {
+    // at least one level: level 0 substitutes the identity for failed votes
+    do {
       const uint32_t mo = (m + 3) / 4;
       uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
       Slab o{base, c->red_cap};
-      k_vm_fold<<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, st>>>(m, c->vm_fold, c->vm_consts, inF, inS, o);
+      k_vm_fold<<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, st>>>(m, c->vm_fold, c->vm_consts, inF, inS, o,
+                                                                       m == n ? d_codes : nullptr);
       inF = o;
       inS = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
       m = mo;
       flip ^= 1;
-    }
+    } while (m > 4);
   }
   HIPCHK(hipGetLastError());
   c->last_n = n;
@@ -1003,7 +985,7 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   if (m > 1) {  // fold the last <= 4 into one partial
     uint32_t* base = c->red + (size_t)(F.p == c->red ? 1 : 0) * PART_PLANES * 12 * c->red_cap;
     Slab o{base, c->red_cap};
-    k_vm_fold<<<1, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o);
+    k_vm_fold<<<1, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o, nullptr);
     F = o;
   }
   // pack element 0 (F planes, S planes) into the AoS partial
@@ -1042,7 +1024,8 @@ int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials)
     const uint32_t mo = (m + 3) / 4;
     uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
     Slab o{base, c->red_cap};
-    k_vm_fold<<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o);
+    k_vm_fold<<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o,
+                                                                            nullptr);
     F = o;
     S = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
     m = mo;

@@ -541,8 +541,10 @@ class Alg:
             if k != nbits - 1:
                 acc = self.pt_dbl(F, acc)
             t = self.pt_add(F, acc, A)
-            bit = p.rbit(k)
-            acc = self.pt_sel(F, bit, acc, t)
+            if F == "fp":
+                acc = tuple(p.selb(k, a_, t_) for a_, t_ in zip(acc, t))
+            else:
+                acc = tuple((p.selb(k, a_[0], t_[0]), p.selb(k, a_[1], t_[1])) for a_, t_ in zip(acc, t))
         return acc
 
     def pt_sel(self, F, f, A, B):

@@ -23,7 +23,7 @@ P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB1
 HALF_P = (P - 1) // 2
 
 HEAVY = {"muls", "sgn0", "lex"}
-LIGHT = {"lin", "sel", "eq", "and", "or", "xor", "rbit"}
+LIGHT = {"lin", "sel", "eq", "and", "or", "xor", "rbit", "st", "selb"}
 
 
 class Val:
@@ -190,6 +190,19 @@ class Prog:
     def rbit(self, k):
         return self._op("rbit", (), (), k)
 
+    def selb(self, k, x, y):
+        """bit k of the unit's 64-bit scalar ? y : x"""
+        if x.id == y.id:
+            return x
+        return self._op("selb", (x.id, y.id), (), k)
+
+    def store(self, name, v, plane):
+        """Write v to output plane `plane` of this unit in HBM (no slot result). The op is a
+        program output so that it is scheduled; its value is v."""
+        st = self._new(Op("st", (v.id,), (), plane, name=name))
+        self.outputs["st:" + name] = st.id
+        return st
+
     # ------------------------------------------------------------------ evaluation
     def evaluate(self, inputs: dict, scalar: int = 0) -> list:
         """Evaluate every value with Python integers (canonical values, not Montgomery)."""
@@ -336,4 +349,8 @@ def eval_op(op, vals, inputs, scalar):
         return vals[s[0]] ^ vals[s[1]]
     if k == "rbit":
         return (scalar >> op.imm) & 1
+    if k == "st":
+        return vals[s[0]]
+    if k == "selb":
+        return vals[s[1]] if (scalar >> op.imm) & 1 else vals[s[0]]
     raise ValueError(k)

@@ -40,9 +40,15 @@ def unflat_g2p(v):
     return (tuple(v[0:2]), tuple(v[2:4]), tuple(v[4:6]))
 
 
+# HBM state planes of a vote (ovhip.hip reads them through VM_S_* in vm_progs.inc)
+S_U, S_FB, S_RS, S_F, S_TOTAL = 0, 4, 16, 22, 34
+
 VOTE_IN = ["pk_x", "pk_sort", "sig_x0", "sig_x1", "sig_sort", "u00", "u01", "u10", "u11"]
-VOTE_OUT = (["pk_ok", "pk_grp", "sig_ok", "sig_grp", "h_inf"] + f12_names("f") + g2p_names("s")
-            + ["pkx", "pky", "sx0", "sx1", "sy0", "sy1"] + g2p_names("h"))
+VOTE_OUT = ["pk_ok", "pk_grp", "sig_ok", "sig_grp", "h_inf"]
+# stored straight to HBM planes by `st` ops as soon as they are final
+VOTE_ST = [(n, S_F + k) for k, n in enumerate(f12_names("f"))] + \
+    [(n, S_RS + k) for k, n in enumerate(g2p_names("s"))] + \
+    [(n, S_FB + k) for k, n in enumerate(["pkx", "pky", "sx0", "sx1", "sy0", "sy1"] + g2p_names("h"))]
 
 
 def build_vote():
@@ -64,10 +70,11 @@ def build_vote():
     rP = a.to_affine("fp", a.pt_mul_rbits("fp", Pp, 64))
     rS = a.pt_mul_rbits("f2", Qs, 64)
     f = a.miller_loop(rP, H)
-    outs = [pk_ok, pk_grp, sig_ok, sig_grp, h_inf] + flat12(f) + flat_g2p(rS) + [px, py, qx[0], qx[1], qy[0], qy[1]] \
-        + flat_g2p(H)
-    for name, v in zip(VOTE_OUT, outs):
+    for name, v in zip(VOTE_OUT, [pk_ok, pk_grp, sig_ok, sig_grp, h_inf]):
         p.output(name, v)
+    stv = flat12(f) + flat_g2p(rS) + [px, py, qx[0], qx[1], qy[0], qy[1]] + flat_g2p(H)
+    for (name, plane), v in zip(VOTE_ST, stv):
+        p.store(name, v, plane)
     return p
 
 

@@ -21,7 +21,7 @@ from collections import defaultdict
 from ir import HALF_P, HEAVY, P
 
 OPC = {"nop": 0, "muls": 1, "sgn0": 2, "lex": 3, "lin": 4, "sel": 5, "eq": 6, "and": 7, "or": 8, "xor": 9,
-       "rbit": 10}
+       "rbit": 10, "st": 11, "selb": 12}
 CONST_BASE = 0x800
 ABSENT = 0xFFFF
 R_MONT = pow(2, 384, P)
@@ -73,7 +73,7 @@ class Scheduled:
                 "cost_est": heavy_rounds * 900 + (self.nrounds - heavy_rounds) * 150}
 
 
-def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1, mixed=True):
+def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1, mixed=True, slot_target=None):
     ops = prog.ops
     live = prog.live_ops()
     liveset = set(live)
@@ -90,45 +90,66 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
     for i in reversed(work):
         c = heavy_w if ops[i].kind in HEAVY else light_w
         prio[i] = c + max((prio[s] for s in succs[i]), default=0)
+        if ops[i].kind == "st":
+            prio[i] = 10 ** 6   # stores free their slot: run them as soon as they are ready
     indeg = {i: len(preds[i]) for i in work}
-    hq, lq = [], []
-
-    def push(i):
-        heapq.heappush(hq if ops[i].kind in HEAVY else lq, (-prio[i], i))
+    # remaining consumers of each slot value (inputs included), for register-pressure control
+    remaining = defaultdict(int)
+    for i in work:
+        for s_ in set(x for x in ops[i].srcs if x is not None and ops[x].kind != "const"):
+            remaining[s_] += 1
+    outset = set(v for v in prog.outputs.values() if ops[v].kind != "st")
+    live_now = sum(1 for i in pre if ops[i].kind == "in")
+    ready_h, ready_l = [], []
     for i in work:
         if indeg[i] == 0:
-            push(i)
-    # Phases: a heavy phase (one Montgomery product per lane) is followed by up to
-    # `max_light` light phases while light ops are ready; results of a phase are visible to
-    # the next phase.
+            (ready_h if ops[i].kind in HEAVY else ready_l).append(i)
+
+    def delta(i):
+        d = 0 if ops[i].kind == "st" else 1
+        for s_ in set(x for x in ops[i].srcs if x is not None and ops[x].kind != "const"):
+            if remaining[s_] == 1 and s_ not in outset:
+                d -= 1
+        return d
+
+    def pick(cands, n, pressure):
+        if not cands or n <= 0:
+            return []
+        if pressure:
+            cands.sort(key=lambda i: (delta(i), -prio[i]))
+        else:
+            cands.sort(key=lambda i: -prio[i])
+        take = cands[:n]
+        del cands[:n]
+        return take
     rounds = []
     kinds = []
     done = 0
     while done < len(work):
-        top_h = -hq[0][0] if hq else -1
-        top_l = -lq[0][0] if lq else -1
-        cur = []
-        if top_l > top_h:
-            # the most critical ready op is light: a cheap light-only phase
+        pressure = slot_target is not None and live_now >= slot_target
+        top_h = max((prio[i] for i in ready_h), default=-1)
+        top_l = max((prio[i] for i in ready_l), default=-1)
+        if top_l > top_h or not ready_h:
             kind = "L"
-            while lq and len(cur) < W:
-                cur.append(heapq.heappop(lq)[1])
+            cur = pick(ready_l, W, pressure)
         else:
-            # heavy phase; idle lanes take light ops (divergent but cheap)
             kind = "H"
-            while hq and len(cur) < W:
-                cur.append(heapq.heappop(hq)[1])
+            cur = pick(ready_h, W, pressure)
             if mixed:
-                while lq and len(cur) < W:
-                    cur.append(heapq.heappop(lq)[1])
+                cur += pick(ready_l, W - len(cur), pressure)
+        if not cur:
+            raise RuntimeError("deadlock in scheduler")
         rounds.append(cur)
         kinds.append(kind)
         done += len(cur)
         for i in cur:
-            for s in succs[i]:
-                indeg[s] -= 1
-                if indeg[s] == 0:
-                    push(s)
+            live_now += delta(i)
+            for s_ in set(x for x in ops[i].srcs if x is not None and ops[x].kind != "const"):
+                remaining[s_] -= 1
+            for s_ in succs[i]:
+                indeg[s_] -= 1
+                if indeg[s_] == 0:
+                    (ready_h if ops[s_].kind in HEAVY else ready_l).append(s_)
     # ---- slot allocation
     def_round = {i: -1 for i in pre if ops[i].kind == "in"}
     for t, r in enumerate(rounds):
@@ -142,7 +163,8 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
                     last_use[s] = max(last_use[s], t)
     end = len(rounds)
     for v in prog.outputs.values():
-        last_use[v] = end
+        if ops[v].kind != "st":
+            last_use[v] = end
     slot_of = {}
     free = []
     nslots = 0
@@ -168,7 +190,8 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
         for s in frees_at.pop(t, []):
             heapq.heappush(free, s)
         for i in r:
-            alloc(i)
+            if ops[i].kind != "st":
+                alloc(i)
     if max_slots is not None and nslots > max_slots:
         raise RuntimeError("%s: %d slots > %d" % (prog.name, nslots, max_slots))
     for i in pre:
@@ -215,9 +238,13 @@ def encode(sc):
                 A, B, C, D = s[0], None, s[1], None
             elif k == "rbit":
                 A = B = C = D = None
+            elif k == "st":
+                A, B, C, D = s[0], None, None, None
+            elif k == "selb":          # B = x, C = y
+                A, B, C, D = None, s[0], s[1], None
             else:
                 raise ValueError(k)
-            w0 = OPC[k] | sb << 5 | sy << 6 | sd << 7 | sc.slot_of[i] << 8 | (op.imm & 63) << 20
+            w0 = OPC[k] | sb << 5 | sy << 6 | sd << 7 | sc.slot_of.get(i, 0) << 8 | (op.imm & 63) << 20
             if k in ("sgn0", "lex"):
                 cref = sc.consts.ref(1, True)   # plain 1: from-Montgomery product
                 w2c = cref
@@ -243,6 +270,7 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
             return val
         return slots[ref]
     W = sc.W
+    stored = {}
     for t in range(sc.nrounds):
         results = []
         for lane in range(W):
@@ -260,6 +288,11 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
                 z = (A & C) if opc == 7 else (A | C) if opc == 8 else (A ^ C)
             elif opc == 10:
                 z = (scalar >> imm) & 1
+            elif opc == 11:
+                stored[imm] = A
+                continue
+            elif opc == 12:
+                z = C if (scalar >> imm) & 1 else B
             else:
                 x = (A - B if sb else A + B) % P
                 y = (C - D if sd else C + D) % P
@@ -278,4 +311,8 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
             results.append((dst, z))
         for dst, z in results:
             slots[dst] = z
-    return {name: slots[sc.slot_of[v]] for name, v in sc.prog.outputs.items()}
+    out = {}
+    for name, v in sc.prog.outputs.items():
+        op = sc.prog.ops[v]
+        out[name] = stored[op.imm] if op.kind == "st" else slots[sc.slot_of[v]]
+    return out

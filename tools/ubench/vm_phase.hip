@@ -1,0 +1,109 @@
+// Microbenchmark of the Fp-VM interpreter on gfx950 (consensus_overlord_amd/csrc/fpvm.hpp):
+// cost of a NOP / LIN / MULS phase at several occupancies, and the latency of a dependent
+// Montgomery product chain without LDS or barriers. Prints one JSON line per case.
+//   hipcc -O3 --offload-arch=gfx950 -o /tmp/vm_phase tools/ubench/vm_phase.hip && /tmp/vm_phase
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <vector>
+
+#include "../../consensus_overlord_amd/csrc/fpvm.hpp"
+
+using namespace ovh;
+
+#define CHECK(x)                                                                   \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e));     \
+      return 1;                                                                    \
+    }                                                                              \
+  } while (0)
+
+constexpr int NSLOT = 64;
+
+__global__ __launch_bounds__(64) void k_vm(const uint4* code, uint32_t nph, uint32_t W, const uint32_t* cst_g,
+                                           uint32_t* out) {
+  __shared__ uint32_t lds[4 * 12 + 4 * NSLOT * 12];
+  uint32_t* cst = lds;
+  if (threadIdx.x < 48) cst[threadIdx.x] = cst_g[threadIdx.x];
+  const uint32_t slice = threadIdx.x / W, lane = threadIdx.x % W;
+  uint32_t* slots = lds + 48 + slice * NSLOT * 12;
+  for (int k = 0; k < 12; ++k) slots[lane * 12 + k] = (k == 0) ? (lane + 3) : (k < 11 ? 0x1234567u * (lane + k) : 0);
+  __syncthreads();
+  vm::run(code, nph, W, lane, true, slots, cst, 0);
+  if (lane == 0) out[blockIdx.x * 64 + threadIdx.x] = slots[0];
+}
+
+__global__ __launch_bounds__(64) void k_chain(uint32_t iters, uint32_t* out) {
+  Fp x, y;
+  for (int k = 0; k < 12; ++k) {
+    x.v[k] = (k < 11) ? 0x9abcdefu * (threadIdx.x + k + 1) : 0;
+    y.v[k] = (k < 11) ? 0x1234567u * (threadIdx.x + k + 7) : 0;
+  }
+  for (uint32_t i = 0; i < iters; ++i) fp_mul(x, x, y);
+  out[blockIdx.x * 64 + threadIdx.x] = x.v[0];
+}
+
+static uint32_t w0(uint32_t op, uint32_t dst) { return op | dst << 8; }
+
+int main() {
+  const uint32_t NPH = 2048;
+  std::vector<uint32_t> cst(48, 0);
+  uint32_t *d_cst, *d_out;
+  CHECK(hipMalloc(&d_cst, 48 * 4));
+  CHECK(hipMemcpy(d_cst, cst.data(), 48 * 4, hipMemcpyHostToDevice));
+  CHECK(hipMalloc(&d_out, 64 * 8192 * 4));
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  const char* names[] = {"nop", "lin", "muls", "muls_half_lanes"};
+  for (uint32_t W : {16u, 64u}) {
+    for (int kind = 0; kind < 4; ++kind) {
+      std::vector<uint32_t> code((size_t)(NPH + 1) * W * 4, 0);
+      for (uint32_t ph = 0; ph < NPH; ++ph)
+        for (uint32_t l = 0; l < W; ++l) {
+          uint32_t* c = &code[((size_t)ph * W + l) * 4];
+          const uint32_t src = (l + 1) % W;
+          if (kind == 1) {
+            c[0] = w0(vm::OP_LIN, l);
+            c[1] = l | src << 16;
+            c[2] = vm::ABSENT | vm::ABSENT << 16;
+          } else if (kind >= 2 && (kind == 2 || l % 2 == 0)) {
+            c[0] = w0(vm::OP_MULS, l);
+            c[1] = l | vm::ABSENT << 16;
+            c[2] = src | vm::ABSENT << 16;
+          }
+        }
+      uint4* d_code;
+      CHECK(hipMalloc(&d_code, code.size() * 4));
+      CHECK(hipMemcpy(d_code, code.data(), code.size() * 4, hipMemcpyHostToDevice));
+      for (uint32_t grid : {256u, 1024u, 2048u, 4096u}) {
+        hipLaunchKernelGGL(k_vm, dim3(grid), dim3(64), 0, 0, d_code, NPH, W, d_cst, d_out);
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipEventRecord(a));
+        hipLaunchKernelGGL(k_vm, dim3(grid), dim3(64), 0, 0, d_code, NPH, W, d_cst, d_out);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        printf("{\"case\": \"vm_%s\", \"W\": %u, \"waves\": %u, \"ms\": %.3f, \"ns_per_phase\": %.1f}\n", names[kind], W,
+               grid, ms, ms * 1e6 / NPH);
+      }
+      CHECK(hipFree(d_code));
+    }
+  }
+  for (uint32_t grid : {256u, 1024u, 2048u, 4096u, 8192u}) {
+    const uint32_t iters = 4096;
+    hipLaunchKernelGGL(k_chain, dim3(grid), dim3(64), 0, 0, iters, d_out);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a));
+    hipLaunchKernelGGL(k_chain, dim3(grid), dim3(64), 0, 0, iters, d_out);
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    printf("{\"case\": \"fp_mul_chain\", \"waves\": %u, \"ms\": %.3f, \"ns_per_mul\": %.1f, \"Mmul_per_s\": %.0f}\n",
+           grid, ms, ms * 1e6 / iters, (double)grid * 64 * iters / (ms * 1e-3) / 1e6);
+  }
+  return 0;
+}
