@@ -32,6 +32,7 @@ SIGNATURES = [
     ("ovh_batch_fallback_device", ctypes.c_int, [_vp, _sz, _vp]),
     ("ovh_stage_times", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_float), _sz]),
     ("ovh_stage_name", ctypes.c_char_p, [ctypes.c_int]),
+    ("ovh_vm_trace", ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), _sz]),
     ("ovh_sign_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp]),
     ("ovh_sk_to_pk_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp]),
 ]

@@ -159,6 +159,7 @@ struct VmDev {  // a program in device memory
   uint32_t nphases;
   const uint16_t* in;   // device copies of the slot maps
   const uint16_t* out;
+  uint64_t* trace;  // OVH_FLAG_VM_TRACE: nphases + 1 timestamps of workgroup 0, else null
 };
 
 #define VM_SLICES 4  // 16-lane slices per 64-lane workgroup
@@ -220,7 +221,8 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, const ui
   }
   __syncthreads();
   vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, i),
-          vm::Out{s.p, s.cap, i});
+          vm::Out{s.p, s.cap, i},
+          blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) {
     const uint32_t pf = hdr[0];
     const uint32_t pk_bad = pf & 1, pk_inf = (pf >> 1) & 1, pk_xz = (pf >> 2) & 1;
@@ -273,7 +275,8 @@ __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const ui
     }
   }
   __syncthreads();
-  vm::run(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  vm::run(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0},
+          blockIdx.x == 0 ? prog.trace : nullptr);
   if (active) {
     for (uint32_t k = lane; k < PART_PLANES; k += VM_FOLD_W) {
       Fp v;
@@ -307,7 +310,8 @@ __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const u
     slot_put(slots, VM_FINAL_IN[k], v.v);
   }
   __syncthreads();
-  vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0},
+          blockIdx.x == 0 ? prog.trace : nullptr);
   if (lane == 0) *result = slot_flag_get(slots, VM_FINAL_OUT[0]) ? 1 : 0;
 }
 
@@ -329,7 +333,8 @@ __global__ __launch_bounds__(64) void k_vm_pairchk(uint32_t n, VmDev prog, const
       slot_put(slots, VM_PAIRCHK_IN[k], v.v);
     }
   __syncthreads();
-  vm::run(prog.code, VM_PAIRCHK_NPHASES, VM_PAIRCHK_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  vm::run(prog.code, VM_PAIRCHK_NPHASES, VM_PAIRCHK_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0},
+          blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) codes[i] = slot_flag_get(slots, VM_PAIRCHK_OUT[0]) ? 0 : BLST_VERIFY_FAIL;
 }
 
@@ -562,6 +567,14 @@ static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphase
   d.nphases = nphases;
   d.in = (const uint16_t*)di;
   d.out = (const uint16_t*)dout;
+  d.trace = nullptr;
+  if (c->flags & OVH_FLAG_VM_TRACE) {
+    void* dt = nullptr;
+    HIPCHK(hipMalloc(&dt, ((size_t)nphases + 1) * 8));
+    c->vm_bufs.push_back(dt);
+    HIPCHK(hipMemset(dt, 0, ((size_t)nphases + 1) * 8));
+    d.trace = (uint64_t*)dt;
+  }
   return 0;
 }
 
@@ -683,6 +696,19 @@ void ovh_destroy(ovh_ctx* c) {
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
   }
   delete c;
+}
+
+int ovh_vm_trace(ovh_ctx* c, int prog, uint64_t* stamps, size_t max) {
+  if (!c || prog < 0 || prog > 3 || (max && !stamps)) return -OVH_ERR_ARG;
+  if (!(c->flags & OVH_FLAG_VM_TRACE)) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess) return -OVH_ERR_DEVICE;
+  const VmDev* d = prog == 0 ? &c->vm_vote : prog == 1 ? &c->vm_fold : prog == 2 ? &c->vm_final : &c->vm_pairchk;
+  const size_t n = (size_t)d->nphases + 1, k = max < n ? max : n;
+  if (hipStreamSynchronize(c->stream) != hipSuccess ||
+      (k && hipMemcpy(stamps, d->trace, k * 8, hipMemcpyDeviceToHost) != hipSuccess))
+    return -OVH_ERR_DEVICE;
+  return (int)n;
 }
 
 int ovh_stage_times(ovh_ctx* c, float* ms, size_t max) {

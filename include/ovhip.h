@@ -41,6 +41,7 @@ typedef struct ovh_ctx ovh_ctx;
 /* Flags for ovh_create. */
 #define OVH_FLAG_AGG_NO_GROUPCHECK 0x1u /* aggregate_signatures without the G2 subgroup check */
 #define OVH_FLAG_PROFILE 0x2u           /* record HIP events around every batch stage */
+#define OVH_FLAG_VM_TRACE 0x4u          /* diagnostics: per-phase clock of the VM kernels' workgroup 0 */
 
 /* Batch stages (ovh_stage_name gives the label). Each stage is one or more kernels enqueued
  * back to back on ovh_stream. */
@@ -112,6 +113,12 @@ int ovh_batch_fallback_device(ovh_ctx* ctx, size_t n, int32_t* d_codes);
  * flag, <0 on error). */
 int ovh_stage_times(ovh_ctx* ctx, float* ms, size_t max);
 const char* ovh_stage_name(int stage);
+
+/* Diagnostics (context created with OVH_FLAG_VM_TRACE): the wall clock (100 MHz counter)
+ * workgroup 0 of the last launch of VM program `prog` (0 vote, 1 fold, 2 final, 3 pairchk)
+ * read after each phase barrier: copies min(max, nphases + 1) stamps, returns nphases + 1
+ * (0 without the flag, <0 on error). */
+int ovh_vm_trace(ovh_ctx* ctx, int prog, uint64_t* stamps, size_t max);
 
 /* Batched helpers used to synthesise workloads on the device. */
 int ovh_sign_batch_device(ovh_ctx* ctx, size_t n, const uint8_t* d_sks, const uint8_t* d_hashes, uint8_t* d_sigs);

@@ -3,8 +3,11 @@
 // product library, never a fallback.
 #include <string.h>
 #include "../../consensus_overlord_amd/csrc/bls/verify.hpp"
+#include "../../consensus_overlord_amd/csrc/fpvm.hpp"
 
 using namespace ovh;
+
+bool ovh::vm::g_host_any = false;
 
 static const uint8_t DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_";
 
@@ -79,6 +82,23 @@ int hx_g1_subgroup(const uint8_t* in, uint32_t len) {
   if (e) return -e;
   G1J j; jac_from_aff(j, a);
   return g1_in_subgroup(j) ? 1 : 0;
+}
+
+// One slice of an Fp-VM program through the interpreter (fpvm.hpp exec), lane by lane in each
+// phase (a phase's writes never target a slot that phase reads: tools/fpvm/sched.py).
+// slots: nslots x 12 words (in/out); planes: `st` output planes, 12 words each.
+// any_all = 1 runs every wave-uniform block for every lane.
+int hx_vm_run(const uint32_t* code, uint32_t nphases, uint32_t W, const uint32_t* cst, uint32_t* slots,
+              uint64_t scalar, uint32_t* planes, uint32_t nplanes, int any_all) {
+  ovh::vm::g_host_any = any_all != 0;
+  const ovh::vm::Out out{planes, 1, 0};
+  (void)nplanes;
+  for (uint32_t ph = 0; ph < nphases; ++ph)
+    for (uint32_t lane = 0; lane < W; ++lane) {
+      const uint32_t* w = code + ((size_t)ph * W + lane) * 4;
+      ovh::vm::exec(uint4{w[0], w[1], w[2], w[3]}, true, slots, cst, scalar, out);
+    }
+  return 0;
 }
 
 }

@@ -1,0 +1,126 @@
+"""The generated Fp-VM programs (tools/fpvm) executed by the interpreter's own code
+(consensus_overlord_amd/csrc/fpvm.hpp exec, host build in tests/host/harness.cpp), compared
+value by value with the slot-level simulator (tools/fpvm/sched.simulate), which gen.py --check
+ties to the CPU oracle on the golden votes. Both interpreter modes: each lane alone, and every
+wave-uniform block run for every lane (what a mixed wave does on the GPU)."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from test_host_harness import hx  # noqa: F401  (module fixture: builds libhx.so)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools", "fpvm"))
+
+import gen  # noqa: E402
+import progs  # noqa: E402
+import sched  # noqa: E402
+from ir import P  # noqa: E402
+
+R = pow(2, 384, P)
+RAW_INPUTS = {"pk_sort", "sig_sort"}   # flags the vote prologue writes as plain limbs
+
+
+def _words(v):
+    return [(v >> (32 * k)) & 0xFFFFFFFF for k in range(12)]
+
+
+def _int(ws):
+    return sum(int(w) << (32 * k) for k, w in enumerate(ws))
+
+
+@pytest.fixture(scope="module")
+def built():
+    return gen.build_all()
+
+
+def run_vm(hx, consts, sc, words, inputs, scalar, any_all):
+    prog = sc.prog
+    slots = np.zeros(sc.nslots * 12, dtype=np.uint32)
+    for name, v in prog.inputs.items():
+        if v in sc.slot_of:
+            val = inputs[name] % P
+            s = sc.slot_of[v]
+            slots[s * 12:s * 12 + 12] = _words(val if name in RAW_INPUTS else val * R % P)
+    code = np.asarray(words, dtype=np.uint32)
+    cst = np.asarray(consts.words(), dtype=np.uint32).ravel()
+    planes = np.zeros(64 * 12, dtype=np.uint32)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    hx.hx_vm_run.argtypes = [u32p, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, ctypes.c_uint64, u32p,
+                             ctypes.c_uint32, ctypes.c_int]
+    assert hx.hx_vm_run(code.ctypes.data_as(u32p), sc.nrounds, sc.W, cst.ctypes.data_as(u32p),
+                        slots.ctypes.data_as(u32p), scalar, planes.ctypes.data_as(u32p), 64, any_all) == 0
+    out = {}
+    for name, v in prog.outputs.items():
+        op = prog.ops[v]
+        if op.kind == "st":
+            out[name] = _int(planes[op.imm * 12:op.imm * 12 + 12])
+        else:
+            s = sc.slot_of[v]
+            out[name] = _int(slots[s * 12:s * 12 + 12])
+    return out
+
+
+def assert_same(dev, sim, what):
+    for name, s in sim.items():
+        d = dev[name]
+        ok = d == s * R % P or (s in (0, 1) and d == s)   # Montgomery value or raw flag
+        assert ok, "%s: output %s interpreter %x, simulator %x" % (what, name, d, s)
+
+
+@pytest.fixture(scope="module")
+def golden_votes():
+    with open(os.path.join(ROOT, "tests", "golden", "golden_v1.json")) as fh:
+        g = json.load(fh)
+    bls = gen._oracle()
+    out = []
+    for v, k in list(zip(g["votes"], g["keys"]))[:2]:
+        out.append(gen.vote_inputs(bls, bytes.fromhex(k["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["digest"])))
+    bad = [c for c in g["verify"] if c["code"] == 3 and len(c["sig"]) == 192 and len(c["pk"]) == 96]
+    for c in bad[:1]:
+        out.append(gen.vote_inputs(bls, bytes.fromhex(c["pk"]), bytes.fromhex(c["sig"]), bytes.fromhex(c["hash"])))
+    return out
+
+
+@pytest.mark.parametrize("any_all", [0, 1])
+def test_vote_program_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
+    consts, progs_ = built
+    prog, sc, words, _, _ = progs_["vote"]
+    r = 0xD7A1C3B5E9F20486
+    for k, inp in enumerate(golden_votes):
+        sim = sched.simulate(sc, words, inp, r)
+        dev = run_vm(hx, consts, sc, words, inp, r, any_all)
+        assert_same(dev, sim, "vote %d" % k)
+
+
+@pytest.mark.parametrize("any_all", [0, 1])
+def test_fold_final_pairchk_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
+    consts, progs_ = built
+    prog, sc, words, _, _ = progs_["vote"]
+    r = 0x1234567890ABCDEF
+    parts = []
+    for inp in golden_votes[:2]:
+        o = sched.simulate(sc, words, inp, r)
+        o = {(n[3:] if n.startswith("st:") else n): v for n, v in o.items()}
+        parts.append(o)
+    inp = {}
+    for k in range(progs.FOLD_K):
+        for j in range(12):
+            inp["F%d_%d" % (k, j)] = parts[k]["f%d" % j] if k < 2 else (1 if j == 0 else 0)
+        for j in range(6):
+            inp["S%d_%d" % (k, j)] = parts[k]["s%d" % j] if k < 2 else (1 if j == 2 else 0)
+    for name in ("fold", "final"):
+        _, psc, pwords, _, _ = progs_[name]
+        sim = sched.simulate(psc, pwords, inp)
+        assert_same(run_vm(hx, consts, psc, pwords, inp, 0, any_all), sim, name)
+        if name == "final":
+            assert sim == {"ok": 1}
+    _, psc, pwords, _, _ = progs_["pairchk"]
+    pin = {n: parts[0][n] for n in progs.PAIRCHK_IN}
+    sim = sched.simulate(psc, pwords, pin)
+    assert sim == {"ok": 1}
+    assert_same(run_vm(hx, consts, psc, pwords, pin, 0, any_all), sim, "pairchk")

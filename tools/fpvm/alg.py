@@ -140,8 +140,9 @@ BETA = _beta()
 
 
 class Alg:
-    def __init__(self, prog: Prog):
+    def __init__(self, prog: Prog, inv_op: bool = False):
         self.p = prog
+        self.inv_op = inv_op   # Fp inversion by the interpreter's one-lane binary Euclid
 
     # ---------------------------------------------------------------- Fp
     def c(self, v):
@@ -179,6 +180,8 @@ class Alg:
         return acc
 
     def fp_inv(self, a):
+        if self.inv_op:
+            return self.p.inv(a)
         return self.fp_pow(a, P - 2)
 
     # ---------------------------------------------------------------- Fp2 (tuples)
@@ -216,6 +219,8 @@ class Alg:
             return (a[0] * p.const(k0), a[1] * p.const(k0))
         if k0 == 0:
             return (-(a[1] * p.const(k1)), a[0] * p.const(k1))
+        if k0 == k1 and k0 <= 15:  # small k (1 + u): linear combinations
+            return (p.lin([(k0, a[0]), (-k0, a[1])]), p.lin([(k0, a[0]), (k0, a[1])]))
         if k0 == k1:  # k0 (1 + u): (a0 - a1) k0 + (a0 + a1) k0 u
             kk = p.const(k0)
             return (p.muls(a[0], -1, a[1], kk, 1, None), p.muls(a[0], 1, a[1], kk, 1, None))
@@ -281,6 +286,40 @@ class Alg:
                     acc = self.f2_sqr(acc)
             acc = odd[val >> 1] if acc is None else self.f2_mul(acc, odd[val >> 1])
             i = j
+        return acc
+
+    def f2_pow_frob(self, a, e: int, w: int = 4):
+        """a^e for e < p^2 with half the squarings of f2_pow: e = e1 p + e0 and a^p = conj(a),
+        so a^e = conj(a)^e1 * a^e0, one shared square chain over max(|e0|, |e1|) bits with
+        sliding windows of width w on both exponents (tables of odd powers of a and conj(a))."""
+        e1, e0 = divmod(e, P)
+        sq = self.f2_sqr(a)
+        odd = [a]
+        for _ in range((1 << (w - 1)) - 1):
+            odd.append(self.f2_mul(odd[-1], sq))
+        odd_c = [self.f2_conj(t) for t in odd]
+
+        def windows(x):   # {bit position: odd window value}, sum(v << pos) == x
+            out, i = {}, x.bit_length() - 1
+            while i >= 0:
+                if not (x >> i) & 1:
+                    i -= 1
+                    continue
+                j = max(i - w + 1, 0)
+                while not (x >> j) & 1:
+                    j += 1
+                out[j] = (x >> j) & ((1 << (i - j + 1)) - 1)
+                i = j - 1
+            return out
+        w0, w1 = windows(e0), windows(e1)
+        acc = None
+        for pos in range(max(e0.bit_length(), e1.bit_length()) - 1, -1, -1):
+            if acc is not None:
+                acc = self.f2_sqr(acc)
+            for wins, tab in ((w0, odd), (w1, odd_c)):
+                if pos in wins:
+                    t = tab[wins[pos] >> 1]
+                    acc = t if acc is None else self.f2_mul(acc, t)
         return acc
 
     def f2_sgn0(self, a):
@@ -402,39 +441,40 @@ class Alg:
         return (self.f2_mul_xi(self.f2_mul(a[2], b1)), self.f2_mul(a[0], b1), self.f2_mul(a[1], b1))
 
     def f12_cyc_sqr(self, a):
-        """Granger-Scott squaring in the cyclotomic subgroup."""
+        """Granger-Scott squaring in the cyclotomic subgroup: three Fp4 squarings
+        (x + y t)^2 = (x^2 + xi y^2) + 2 x y t, each from 7 Fp products whose operands are 2-term
+        sums, and every output coefficient one 4-term linear combination (3 t -/+ 2 z)."""
+        p = self.p
         r0, r4, r3 = a[0]
         r2, r1, r5 = a[1]
 
-        def fp4_sqr(x, y):
-            tmp = self.f2_mul(x, y)
-            t0 = self.f2_sub(self.f2_sub(self.f2_mul(self.f2_add(x, y), self.f2_add(self.f2_mul_xi(y), x)), tmp),
-                             self.f2_mul_xi(tmp))
-            return t0, self.f2_dbl(tmp)
-        t0, t1 = fp4_sqr(r0, r1)
-        t2, t3 = fp4_sqr(r2, r3)
-        t4, t5 = fp4_sqr(r4, r5)
-        p = self.p
+        def fp4_sqr_terms(x, y):
+            X0 = p.muls(x[0], 1, x[1], x[0], -1, x[1])      # (x0 + x1)(x0 - x1)
+            X1 = p.muls(x[0], 1, x[0], x[1], 1, None)       # 2 x0 x1
+            Y0 = p.muls(y[0], 1, y[1], y[0], -1, y[1])
+            Y1 = p.muls(y[0], 1, y[0], y[1], 1, None)
+            P0 = x[0] * y[0]
+            P1 = x[1] * y[1]
+            P2 = p.muls(x[0], 1, x[1], y[0], 1, y[1])
+            # t0 = x^2 + xi y^2 = (X0 + Y0 - Y1, X1 + Y0 + Y1); t1 = 2 x y = (2P0 - 2P1, 2P2 - 2P0 - 2P1)
+            t0 = ([(1, X0), (1, Y0), (-1, Y1)], [(1, X1), (1, Y0), (1, Y1)])
+            t1 = ([(2, P0), (-2, P1)], [(2, P2), (-2, P0), (-2, P1)])
+            return t0, t1
 
-        def three_minus_two(t, z):  # 3t - 2z = 2 (t - z) + t
-            out = []
-            for ti, zi in zip(t, z):
-                d = p.lin4(ti, -1, zi, 1, None)
-                out.append(p.lin4(d, 1, d, 1, ti))
-            return tuple(out)
-
-        def three_plus_two(t, z):  # 3t + 2z = 2 (t + z) + t
-            out = []
-            for ti, zi in zip(t, z):
-                d = p.lin4(ti, 1, zi, 1, None)
-                out.append(p.lin4(d, 1, d, 1, ti))
-            return tuple(out)
-        z0 = three_minus_two(t0, r0)
-        z1 = three_plus_two(t1, r1)
-        z2 = three_plus_two(self.f2_mul_xi(t5), r2)
-        z3 = three_minus_two(t4, r3)
-        z4 = three_minus_two(t2, r4)
-        z5 = three_plus_two(t3, r5)
+        def comb(t, z, sign):  # 3 t + sign 2 z, componentwise
+            return tuple(p.lin([(3 * c, v) for c, v in ti] + [(2 * sign, zi)]) for ti, zi in zip(t, z))
+        t0, t1 = fp4_sqr_terms(r0, r1)
+        t2, t3 = fp4_sqr_terms(r2, r3)
+        t4, t5 = fp4_sqr_terms(r4, r5)
+        # xi t5 = (t5.c0 - t5.c1, t5.c0 + t5.c1)
+        xt5 = ([(c, v) for c, v in t5[0]] + [(-c, v) for c, v in t5[1]],
+               [(c, v) for c, v in t5[0]] + [(c, v) for c, v in t5[1]])
+        z0 = comb(t0, r0, -1)
+        z1 = comb(t1, r1, 1)
+        z2 = comb(xt5, r2, 1)
+        z3 = comb(t4, r3, -1)
+        z4 = comb(t2, r4, -1)
+        z5 = comb(t3, r5, 1)
         return ((z0, z4, z3), (z2, z1, z5))
 
     def f12_eq_one(self, a):
@@ -619,7 +659,7 @@ class Alg:
         tv3 = self.f2_sqr(tv2)
         tv3 = self.f2_mul(tv3, v)
         tv5 = self.f2_mul(u, tv3)
-        tv5 = self.f2_pow(tv5, SR_C3)
+        tv5 = self.f2_pow_frob(tv5, SR_C3)
         tv5 = self.f2_mul(tv5, tv2)
         tv2 = self.f2_mul(tv5, v)
         tv3 = self.f2_mul(tv5, u)

@@ -5,25 +5,31 @@ onto the lanes of a wave slice (sched.py).
 Every value is one Fp element (a "slot" at run time). Flags are Fp slots holding 0/1 in limb 0.
 Operations (the interpreter in consensus_overlord_amd/csrc/fpvm.hpp implements exactly these):
 
-  muls  z = (a + sb*b) * (c + sd*d)            heavy: one Montgomery product
+  muls  z = (ca a + cb b) * (cc c + cd d)      heavy: one Montgomery product
   sgn0  z = parity(canonical(a))               heavy (from-Montgomery product)
   lex   z = canonical(a) > (p-1)/2             heavy
-  lin   z = (a + sb*b) + sy*(c + sd*d)         light
+  inv   z = a^-1 (0 -> 0)                      heavy+: binary extended Euclid in one lane
+  lin   z = ca a + cb b + cc c + cd d          light
+  eq    z = (ca a + cb b) == (cc c + cd d)     light
   sel   z = flag(f) ? y : x                    light
-  eq    z = (a + sb*b) == (c + sd*d)           light
-  and/or/xor  on flags                          light
-  rbit  z = bit k of the vote's 64-bit scalar   light
+  selb  z = bit k of the unit's scalar ? y : x light
+  and/or/xor  on flags                         light
+  st    store a to the unit's output plane k   light (no result slot)
 
-Signs are +1 / -1; a missing operand is None. Constants are Fp values referenced by index
-into a constant table; inputs are named slots the prologue fills.
+Coefficients are small signed integers (|c| <= CMAX); a missing operand has coefficient 0.
+Constants are Fp values referenced by index into a constant table; inputs are named slots the
+prologue fills.
 """
 from __future__ import annotations
 
+import math
+
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 HALF_P = (P - 1) // 2
+CMAX = 15
 
-HEAVY = {"muls", "sgn0", "lex"}
-LIGHT = {"lin", "sel", "eq", "and", "or", "xor", "rbit", "st", "selb"}
+HEAVY = {"muls", "sgn0", "lex", "inv"}
+LIGHT = {"lin", "sel", "eq", "and", "or", "xor", "st", "selb"}
 
 
 class Val:
@@ -33,29 +39,79 @@ class Val:
         self.prog = prog
         self.id = vid
 
-    # arithmetic sugar (Fp)
     def __add__(self, o):
-        return self.prog.lin(self, o, 1)
+        return self.prog.lin([(1, self), (1, o)])
 
     def __sub__(self, o):
-        return self.prog.lin(self, o, -1)
+        return self.prog.lin([(1, self), (-1, o)])
 
     def __mul__(self, o):
         return self.prog.mul(self, o)
 
     def __neg__(self):
-        return self.prog.lin(self.prog.zero, self, -1)
+        return self.prog.lin([(-1, self)])
 
 
 class Op:
-    __slots__ = ("kind", "srcs", "signs", "imm", "name")
+    __slots__ = ("kind", "srcs", "coefs", "imm", "name")
 
-    def __init__(self, kind, srcs=(), signs=(), imm=0, name=None):
+    def __init__(self, kind, srcs=(), coefs=(), imm=0, name=None):
         self.kind = kind
-        self.srcs = tuple(srcs)    # value ids (or None) -- order (a, b, c, d) / (f, x, y)
-        self.signs = tuple(signs)  # (sb, sy, sd) for lin/muls/eq
+        self.srcs = tuple(srcs)    # value ids or None; (a, b, c, d) for muls/lin/eq
+        self.coefs = tuple(coefs)  # (ca, cb, cc, cd) for muls/lin/eq
         self.imm = imm
         self.name = name
+
+
+def _norm_terms(terms):
+    """[(coef, id)] -> merged, zero-free list"""
+    acc = {}
+    order = []
+    for c, v in terms:
+        if v not in acc:
+            acc[v] = 0
+            order.append(v)
+        acc[v] += c
+    return [(acc[v], v) for v in order if acc[v] != 0]
+
+
+def _expand_unit(terms, width):
+    """[(c, v)] -> <= width (sign, v) unit terms, first sign +1 (v None = the zero constant),
+    or None. c * v becomes |c| copies of (sign c, v)."""
+    ex = []
+    for c, v in terms:
+        ex += [(1 if c > 0 else -1, v)] * abs(c)
+    if not ex:
+        return [(1, None)]
+    pos = [t for t in ex if t[0] > 0]
+    neg = [t for t in ex if t[0] < 0]
+    if pos:
+        ex = pos[:1] + pos[1:] + neg
+    else:
+        ex = [(1, None)] + neg          # 0 - a - b ...
+    return ex if len(ex) <= width else None
+
+
+def lin_form(terms, width=4):
+    """How the interpreter evaluates sum c_i v_i (fpvm.hpp exec):
+    ("unit", u)      u = <= width unit terms, plain modular adds / subs;
+    ("scaled", k, u) k * (unit sum), 2 <= k <= 15: one small-scalar product + reduction;
+    ("acc", terms)   general signed 13-limb accumulation + reduction (slow)."""
+    terms = [(c, v) for c, v in terms if c]
+    u = _expand_unit(terms, width)
+    if u is not None:
+        return ("unit", u)
+    g = 0
+    for c, _ in terms:
+        g = math.gcd(g, abs(c))
+    if 2 <= g <= CMAX:
+        u = _expand_unit([(c // g, v) for c, v in terms], width)
+        if u is not None:
+            return ("scaled", g, u)
+    return ("acc", terms)
+
+
+FORM_COST = {"unit": 1, "scaled": 2, "acc": 6}
 
 
 class Prog:
@@ -64,13 +120,13 @@ class Prog:
     def __init__(self, name):
         self.name = name
         self.ops = []
-        self.outputs = {}       # name -> value id
-        self.inputs = {}        # name -> value id
-        self._consts = {}       # int -> value id
-        self.zero = self.const(0)
-        self.one = self.const(1)  # the field element 1 (Montgomery R at run time)
+        self.outputs = {}
+        self.inputs = {}
+        self._consts = {}
         self.cse = {}
-        self.raw_one = self.raw_const(1)  # raw limbs [1, 0, ...]: the flag "true" / plain 1
+        self.zero = self.const(0)
+        self.one = self.const(1)          # the field element 1 (Montgomery R at run time)
+        self.raw_one = self.raw_const(1)  # raw limbs [1, 0, ...]: flag "true" / plain 1
 
     # ------------------------------------------------------------------ builders
     def _new(self, op):
@@ -102,14 +158,11 @@ class Prog:
     def output(self, name, v: Val):
         self.outputs[name] = v.id
 
-    def _key(self, kind, srcs, signs, imm=0):
-        return (kind, srcs, signs, imm)
-
-    def _op(self, kind, srcs, signs=(), imm=0):
-        k = self._key(kind, srcs, signs, imm)
+    def _op(self, kind, srcs, coefs=(), imm=0):
+        k = (kind, tuple(srcs), tuple(coefs), imm)
         if k in self.cse:
             return Val(self, self.cse[k])
-        v = self._new(Op(kind, srcs, signs, imm))
+        v = self._new(Op(kind, srcs, coefs, imm))
         self.cse[k] = v.id
         return v
 
@@ -120,42 +173,75 @@ class Prog:
     def cval(self, v):
         return self.ops[v.id].imm
 
-    def lin(self, a, b, sb=1):
-        """a + sb*b"""
-        if self.is_const(b) and self.cval(b) == 0:
-            return a
-        if self.is_const(a) and self.cval(a) == 0 and sb == 1:
-            return b
-        if self.is_const(a) and self.is_const(b):
-            return self.const(self.cval(a) + sb * self.cval(b))
-        return self._op("lin", (a.id, b.id, None, None), (sb, 1, 1))
+    def lin(self, terms):
+        """sum of coef * value, terms = [(coef, Val)] (any length; chained in 4-term ops)."""
+        t = []
+        cacc = 0
+        for c, v in terms:
+            if self.is_const(v):
+                cacc += c * self.cval(v)
+            else:
+                t.append((c, v.id))
+        t = _norm_terms(t)
+        cacc %= P
+        if cacc:
+            t.append((1, self.const(cacc).id))
+        if not t:
+            return self.zero
+        if len(t) == 1 and t[0][0] == 1:
+            return Val(self, t[0][1])
+        out = None
+        while t:
+            n = 4 if out is None else 3
+            chunk, t = t[:n], t[n:]
+            if out is not None:
+                chunk = [(1, out.id)] + chunk
+            fixed = []
+            for c, v in chunk:
+                if abs(c) > CMAX:
+                    v = self.mul(Val(self, v), self.const(abs(c))).id
+                    c = 1 if c > 0 else -1
+                fixed.append((c, v))
+            chunk = sorted(fixed, key=lambda cv: cv[1])
+            srcs = [v for _, v in chunk] + [None] * (4 - len(chunk))
+            coefs = [c for c, _ in chunk] + [0] * (4 - len(chunk))
+            out = self._op("lin", srcs, coefs)
+        return out
 
     def lin4(self, a, sb, b, sy, c, sd=1, d=None):
         """(a + sb*b) + sy*(c + sd*d); b, c, d may be None."""
-        return self._op("lin", (a.id, b.id if b is not None else None, c.id if c is not None else None,
-                                d.id if d is not None else None), (sb, sy, sd))
+        t = [(1, a)]
+        if b is not None:
+            t.append((sb, b))
+        if c is not None:
+            t.append((sy, c))
+        if d is not None:
+            t.append((sy * sd, d))
+        return self.lin(t)
 
     def mul(self, a, b):
         if self.is_const(a) and not self.is_const(b):
             a, b = b, a
         if self.is_const(b):
             cv = self.cval(b)
+            if self.is_const(a):
+                return self.const(self.cval(a) * cv)
             if cv == 0:
                 return self.zero
             if cv == 1:
                 return a
-            if cv == 2:
-                return self.lin(a, a, 1)
-            if cv == P - 1:
-                return self.lin(self.zero, a, -1)
+            if cv <= CMAX:
+                return self.lin([(cv, a)])
+            if P - cv <= CMAX:
+                return self.lin([(-(P - cv), a)])
         if a.id > b.id and not self.is_const(b):
             a, b = b, a
-        return self._op("muls", (a.id, None, b.id, None), (1, 1, 1))
+        return self._op("muls", (a.id, None, b.id, None), (1, 0, 1, 0))
 
     def muls(self, a, sb, b, c, sd, d):
         """(a + sb*b) * (c + sd*d); b or d may be None."""
         return self._op("muls", (a.id, b.id if b is not None else None, c.id, d.id if d is not None else None),
-                        (sb, 1, sd))
+                        (1, sb if b is not None else 0, 1, sd if d is not None else 0))
 
     def sgn0(self, a):
         return self._op("sgn0", (a.id,))
@@ -163,8 +249,11 @@ class Prog:
     def lex(self, a):
         return self._op("lex", (a.id,))
 
+    def inv(self, a):
+        return self._op("inv", (a.id,))
+
     def eq(self, a, b):
-        return self._op("eq", (a.id, None, b.id, None), (1, 1, 1))
+        return self._op("eq", (a.id, None, b.id, None), (1, 0, 1, 0))
 
     def is_zero(self, a):
         return self.eq(a, self.zero)
@@ -174,6 +263,12 @@ class Prog:
         if x.id == y.id:
             return x
         return self._op("sel", (f.id, x.id, y.id))
+
+    def selb(self, k, x, y):
+        """bit k of the unit's 64-bit scalar ? y : x"""
+        if x.id == y.id:
+            return x
+        return self._op("selb", (x.id, y.id), (), k)
 
     def f_and(self, a, b):
         return self._op("and", (a.id, b.id))
@@ -187,65 +282,19 @@ class Prog:
     def f_not(self, a):
         return self.f_xor(a, self.raw_one)
 
-    def rbit(self, k):
-        return self._op("rbit", (), (), k)
-
-    def selb(self, k, x, y):
-        """bit k of the unit's 64-bit scalar ? y : x"""
-        if x.id == y.id:
-            return x
-        return self._op("selb", (x.id, y.id), (), k)
-
     def store(self, name, v, plane):
-        """Write v to output plane `plane` of this unit in HBM (no slot result). The op is a
-        program output so that it is scheduled; its value is v."""
+        """Write v to output plane `plane` of this unit in HBM (no slot result)."""
         st = self._new(Op("st", (v.id,), (), plane, name=name))
         self.outputs["st:" + name] = st.id
         return st
 
-    # ------------------------------------------------------------------ evaluation
-    def evaluate(self, inputs: dict, scalar: int = 0) -> list:
-        """Evaluate every value with Python integers (canonical values, not Montgomery)."""
-        vals = [None] * len(self.ops)
-        for i, op in enumerate(self.ops):
-            vals[i] = eval_op(op, vals, inputs, scalar)
-        return vals
-
     # ------------------------------------------------------------------ optimisation
-    def _terms(self, op):
-        """signed terms of a lin op: [(sign, value id)]"""
-        sb, sy, sd = op.signs
-        a, b, c, d = op.srcs
-        t = [(1, a)]
-        if b is not None:
-            t.append((sb, b))
-        if c is not None:
-            t.append((sy, c))
-        if d is not None:
-            t.append((sy * sd, d))
-        return t
-
-    @staticmethod
-    def _pack(terms):
-        """4 signed terms -> (srcs, signs) in (A + sb B) + sy (C + sd D) form, or None."""
-        terms = sorted(terms, key=lambda t: -t[0])  # a positive term first
-        if terms[0][0] < 0 or len(terms) > 4:
-            return None
-        (s1, a), rest = terms[0], terms[1:]
-        b = c = d = None
-        sb = sy = sd = 1
-        if len(rest) >= 1:
-            sb, b = rest[0]
-        if len(rest) >= 2:
-            sy, c = rest[1]
-        if len(rest) >= 3:
-            sd = rest[2][0] * sy
-            d = rest[2][1]
-        return (a, b, c, d), (sb, sy, sd)
+    def _lin_terms(self, op):
+        return [(c, v) for c, v in zip(op.coefs, op.srcs) if v is not None and c != 0]
 
     def fuse(self):
-        """Merge single-use lin chains into 4-term lin ops, and single-use 2-term lins into the
-        pre-additions of muls / eq operands. Returns the number of ops absorbed."""
+        """Merge single-use lin ops into their consumer: into a lin (<= 4 distinct terms, small
+        coefficients) or into the 2-term operand sums of muls / eq. Returns ops absorbed."""
         live = set(self.live_ops())
         outs = set(self.outputs.values())
         uses = [0] * len(self.ops)
@@ -255,49 +304,52 @@ class Prog:
                     uses[s] += 1
         absorbed = 0
 
+        def cost(terms, limit):
+            f = lin_form(terms, limit)[0]
+            return FORM_COST[f] if limit == 4 else (0 if f == "unit" else 1000)  # muls operands: unit only
+
         def fusable(j):
-            o = self.ops[j]
-            return o.kind == "lin" and uses[j] == 1 and j not in outs
+            return j is not None and self.ops[j].kind == "lin" and uses[j] == 1 and j not in outs
+
+        def try_merge(terms, limit):
+            nonlocal absorbed
+            changed = True
+            while changed:
+                changed = False
+                for k, (c, v) in enumerate(terms):
+                    if fusable(v):
+                        sub = [(c * c2, v2) for c2, v2 in self._lin_terms(self.ops[v])]
+                        cand = _norm_terms(terms[:k] + terms[k + 1:] + sub)
+                        if len(cand) <= limit and all(abs(c3) <= CMAX for c3, _ in cand) and \
+                                cost(cand, limit) <= cost(terms, limit) + cost(self._lin_terms(self.ops[v]), 4):
+                            uses[v] -= 1
+                            for _, v2 in sub:
+                                uses[v2] += 1
+                            terms[:] = cand
+                            absorbed += 1
+                            changed = True
+                            break
+            return terms
         for i in sorted(live):
             op = self.ops[i]
             if op.kind == "lin":
-                terms = self._terms(op)
-                changed = True
-                while changed:
-                    changed = False
-                    for k, (sg, v) in enumerate(terms):
-                        if v is not None and fusable(v):
-                            sub = [(sg * s2, v2) for s2, v2 in self._terms(self.ops[v])]
-                            cand = terms[:k] + terms[k + 1:] + sub
-                            packed = self._pack(cand) if len(cand) <= 4 else None
-                            if packed is not None:
-                                terms = cand
-                                uses[v] -= 1
-                                for _, v2 in sub:
-                                    uses[v2] += 1
-                                absorbed += 1
-                                changed = True
-                                break
-                srcs, signs = self._pack(terms)
-                op.srcs, op.signs = srcs, signs
+                terms = try_merge(self._lin_terms(op), 4)
+                terms = sorted(terms, key=lambda cv: cv[1])
+                op.srcs = tuple([v for _, v in terms] + [None] * (4 - len(terms)))
+                op.coefs = tuple([c for c, _ in terms] + [0] * (4 - len(terms)))
             elif op.kind in ("muls", "eq"):
-                sb, sy, sd = op.signs
                 a, b, c, d = op.srcs
-                new = [a, b, c, d]
-                sg = [1, sb, 1, sd]
-                for half in (0, 2):
-                    x, y = new[half], new[half + 1]
-                    if y is None and x is not None and fusable(x):
-                        t = self._terms(self.ops[x])
-                        if len(t) == 2 and t[0][0] == 1:
-                            uses[x] -= 1
-                            new[half], new[half + 1] = t[0][1], t[1][1]
-                            sg[half + 1] = t[1][0]
-                            uses[t[0][1]] += 1
-                            uses[t[1][1]] += 1
-                            absorbed += 1
-                op.srcs = tuple(new)
-                op.signs = (sg[1], sy, sg[3])
+                ca, cb, cc, cd = op.coefs
+                left = try_merge(_norm_terms([(ca, a)] + ([(cb, b)] if b is not None and cb else [])), 2)
+                right = try_merge(_norm_terms([(cc, c)] + ([(cd, d)] if d is not None and cd else [])), 2)
+                if not left:
+                    left = [(1, self.zero.id)]
+                if not right:
+                    right = [(1, self.zero.id)]
+                left = left + [(0, None)] * (2 - len(left))
+                right = right + [(0, None)] * (2 - len(right))
+                op.srcs = (left[0][1], left[1][1], right[0][1], right[1][1])
+                op.coefs = (left[0][0], left[1][0], right[0][0], right[1][0])
         self.cse = {}
         return absorbed
 
@@ -315,6 +367,14 @@ class Prog:
                     stack.append(s)
         return sorted(need)
 
+    # ------------------------------------------------------------------ evaluation
+    def evaluate(self, inputs: dict, scalar: int = 0) -> list:
+        """Evaluate every value with Python integers (canonical values, not Montgomery)."""
+        vals = [None] * len(self.ops)
+        for i, op in enumerate(self.ops):
+            vals[i] = eval_op(op, vals, inputs, scalar)
+        return vals
+
 
 def eval_op(op, vals, inputs, scalar):
     k = op.kind
@@ -327,30 +387,30 @@ def eval_op(op, vals, inputs, scalar):
     def g(i):
         return 0 if s[i] is None else vals[s[i]]
     if k in ("muls", "lin", "eq"):
-        sb, sy, sd = op.signs
-        x = (g(0) + sb * g(1)) % P
-        y = (g(2) + sd * g(3)) % P
+        ca, cb, cc, cd = op.coefs
+        if k == "lin":
+            return (ca * g(0) + cb * g(1) + cc * g(2) + cd * g(3)) % P
+        x = (ca * g(0) + cb * g(1)) % P
+        y = (cc * g(2) + cd * g(3)) % P
         if k == "muls":
             return x * y % P
-        if k == "lin":
-            return (x + sy * y) % P
         return 1 if x == y else 0
     if k == "sgn0":
         return vals[s[0]] & 1
     if k == "lex":
         return 1 if vals[s[0]] > HALF_P else 0
+    if k == "inv":
+        return pow(vals[s[0]], P - 2, P)
     if k == "sel":
         return vals[s[2]] if vals[s[0]] else vals[s[1]]
+    if k == "selb":
+        return vals[s[1]] if (scalar >> op.imm) & 1 else vals[s[0]]
     if k == "and":
         return vals[s[0]] & vals[s[1]]
     if k == "or":
         return vals[s[0]] | vals[s[1]]
     if k == "xor":
         return vals[s[0]] ^ vals[s[1]]
-    if k == "rbit":
-        return (scalar >> op.imm) & 1
     if k == "st":
         return vals[s[0]]
-    if k == "selb":
-        return vals[s[1]] if (scalar >> op.imm) & 1 else vals[s[0]]
     raise ValueError(k)

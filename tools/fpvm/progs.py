@@ -107,7 +107,7 @@ FINAL_OUT = ["ok"]
 
 def build_final():
     p = Prog("final")
-    a = Alg(p)
+    a = Alg(p, inv_op=True)
     Fs, Ss = [], []
     for k in range(FOLD_K):
         Fs.append(unflat12([p.input(n) for n in f12_names("F%d_" % k)]))

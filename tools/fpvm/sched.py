@@ -2,26 +2,28 @@
 per-lane instruction stream, and re-execute the encoded stream slot by slot (simulate) to
 prove scheduling + allocation preserve the program's values.
 
-Round semantics (the interpreter, consensus_overlord_amd/csrc/fpvm.hpp): in round t every lane
+Phase semantics (the interpreter, consensus_overlord_amd/csrc/fpvm.hpp): in phase t every lane
 of a slice reads its operands from LDS slots / the constant table, computes one op and writes
-one slot; results are visible from round t + 1. A slot whose value was last read in round t can
-be rewritten from round t + 1 on.
+one slot; results are visible from phase t + 1. A slot whose value was last read in phase t can
+be rewritten from phase t + 1 on.
 
-Instruction (4 x uint32 per lane per round):
-  w0 = opcode | sb << 5 | sy << 6 | sd << 7 | dst << 8 (11 bits) | imm << 20 (6 bits)
-  w1 = A | B << 16,  w2 = C | D << 16,  w3 = 0
-  operand: slot index (< CONST_BASE), CONST_BASE + k (constant table entry k), ABSENT (zero)
-  signs: 0 = +, 1 = -.
+Instruction (4 x uint32 per lane per phase):
+  w0 = opcode | dst << 5 (11 bits) | imm << 16 (6 bits)
+  w1 = A | B << 16,  w2 = C | D << 16
+  w3 = ca | cb << 5 | cc << 10 | cd << 15   (5-bit two's-complement coefficients)
+       | k << 20 (lin: k * (unit sum) when 2 <= k <= 15, ir.lin_form "scaled")
+  operand: slot index (< CONST_BASE) or CONST_BASE + k (constant table entry k); a missing
+  operand is the zero constant with coefficient 0, so every lane loads four operands.
 """
 from __future__ import annotations
 
 import heapq
 from collections import defaultdict
 
-from ir import HALF_P, HEAVY, P
+from ir import CMAX, HALF_P, HEAVY, P, lin_form
 
-OPC = {"nop": 0, "muls": 1, "sgn0": 2, "lex": 3, "lin": 4, "sel": 5, "eq": 6, "and": 7, "or": 8, "xor": 9,
-       "rbit": 10, "st": 11, "selb": 12}
+OPC = {"nop": 0, "muls": 1, "sgn0": 2, "lex": 3, "inv": 4, "lin": 5, "sel": 6, "eq": 7, "and": 8, "or": 9,
+       "xor": 10, "st": 11, "selb": 12}
 CONST_BASE = 0x800
 ABSENT = 0xFFFF
 R_MONT = pow(2, 384, P)
@@ -204,15 +206,20 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
 
 def _operand(sc, v):
     if v is None:
-        return ABSENT
+        return sc.consts.ref(0, False)
     op = sc.prog.ops[v]
     if op.kind == "const":
         return sc.consts.ref(op.imm, op.name == "raw")
     return sc.slot_of[v]
 
 
+def _c5(c):
+    assert -16 <= c <= 15
+    return c & 31
+
+
 def encode(sc):
-    """-> list of uint32 words, nrounds * W * 4."""
+    """-> list of uint32 words, nphases * W * 4."""
     words = []
     ops = sc.prog.ops
     for r in sc.rounds:
@@ -224,34 +231,62 @@ def encode(sc):
             op = ops[i]
             k = op.kind
             s = list(op.srcs) + [None] * (4 - len(op.srcs))
-            sb = sy = sd = 0
-            if k in ("muls", "lin", "eq"):
-                sb = 1 if op.signs[0] < 0 else 0
-                sy = 1 if op.signs[1] < 0 else 0
-                sd = 1 if op.signs[2] < 0 else 0
-                A, B, C, D = s[0], s[1], s[2], s[3]
+            coefs = (0, 0, 0, 0)
+            scale = 0
+            if k == "lin":
+                form = lin_form(sc.prog._lin_terms(op), 4)
+                if form[0] == "acc":
+                    A, B, C, D = s
+                    coefs = op.coefs
+                else:
+                    u = form[-1] + [(0, None)] * (4 - len(form[-1]))
+                    A, B, C, D = (v for _, v in u)
+                    coefs = tuple(c for c, _ in u)
+                    if form[0] == "scaled":
+                        scale = form[1]
+            elif k in ("muls", "eq"):
+                A, B, C, D = s
+                coefs = list(op.coefs)
+                for h in (0, 2):
+                    terms = [(c, v) for c, v in zip(op.coefs[h:h + 2], s[h:h + 2]) if v is not None and c]
+                    form = lin_form(terms, 2)
+                    assert form[0] == "unit", (k, op.coefs)   # the interpreter's muls operands are unit sums
+                    if form[0] == "unit":
+                        u = form[1] + [(0, None)] * (2 - len(form[1]))
+                        if h == 0:
+                            A, B = u[0][1], u[1][1]
+                        else:
+                            C, D = u[0][1], u[1][1]
+                        coefs[h], coefs[h + 1] = u[0][0], u[1][0]
             elif k in ("sgn0", "lex"):
                 A, B, C, D = s[0], None, None, None
+                coefs = (1, 0, 1, 0)
+            elif k in ("inv", "st"):
+                A, B, C, D = s[0], None, None, None
+                coefs = (1, 0, 0, 0)
             elif k == "sel":           # A = flag, B = x, C = y
                 A, B, C, D = s[0], s[1], s[2], None
-            elif k in ("and", "or", "xor"):
-                A, B, C, D = s[0], None, s[1], None
-            elif k == "rbit":
-                A = B = C = D = None
-            elif k == "st":
-                A, B, C, D = s[0], None, None, None
             elif k == "selb":          # B = x, C = y
                 A, B, C, D = None, s[0], s[1], None
+            elif k in ("and", "or", "xor"):
+                A, B, C, D = s[0], None, s[1], None
             else:
                 raise ValueError(k)
-            w0 = OPC[k] | sb << 5 | sy << 6 | sd << 7 | sc.slot_of.get(i, 0) << 8 | (op.imm & 63) << 20
+            dst = sc.slot_of.get(i, 0)
+            w0 = OPC[k] | dst << 5 | (op.imm & 63) << 16
             if k in ("sgn0", "lex"):
-                cref = sc.consts.ref(1, True)   # plain 1: from-Montgomery product
-                w2c = cref
+                cref = sc.consts.ref(1, True)          # plain 1: from-Montgomery product
+            elif k == "inv":
+                cref = sc.consts.ref(R_MONT * R_MONT % P, False)   # raw R^3: back to Montgomery
             else:
-                w2c = _operand(sc, C)
-            words += [w0, _operand(sc, A) | _operand(sc, B) << 16, w2c | _operand(sc, D) << 16, 0]
+                cref = _operand(sc, C)
+            w3 = _c5(coefs[0]) | _c5(coefs[1]) << 5 | _c5(coefs[2]) << 10 | _c5(coefs[3]) << 15 | scale << 20
+            words += [w0, _operand(sc, A) | _operand(sc, B) << 16, cref | _operand(sc, D) << 16, w3]
     return words
+
+
+def _s5(x):
+    return x - 32 if x & 16 else x
 
 
 def simulate(sc, words, inputs: dict, scalar: int = 0):
@@ -263,48 +298,47 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
             slots[sc.slot_of[v]] = inputs[name] % P
 
     def get(ref):
-        if ref == ABSENT:
-            return 0
         if ref >= CONST_BASE:
-            val, raw = const_vals[ref - CONST_BASE]
-            return val
+            return const_vals[ref - CONST_BASE][0]
         return slots[ref]
     W = sc.W
     stored = {}
     for t in range(sc.nrounds):
         results = []
         for lane in range(W):
-            w0, w1, w2, _ = words[(t * W + lane) * 4:(t * W + lane) * 4 + 4]
+            w0, w1, w2, w3 = words[(t * W + lane) * 4:(t * W + lane) * 4 + 4]
             opc = w0 & 31
             if opc == 0:
                 continue
-            sb, sy, sd = (w0 >> 5) & 1, (w0 >> 6) & 1, (w0 >> 7) & 1
-            dst = (w0 >> 8) & 0x7FF
-            imm = (w0 >> 20) & 63
+            dst = (w0 >> 5) & 0x7FF
+            imm = (w0 >> 16) & 63
             A, B, C, D = get(w1 & 0xFFFF), get(w1 >> 16), get(w2 & 0xFFFF), get(w2 >> 16)
-            if opc == 5:
+            ca, cb, cc, cd = (_s5((w3 >> (5 * q)) & 31) for q in range(4))
+            if opc == OPC["sel"]:
                 z = C if A else B
-            elif opc in (7, 8, 9):
-                z = (A & C) if opc == 7 else (A | C) if opc == 8 else (A ^ C)
-            elif opc == 10:
-                z = (scalar >> imm) & 1
-            elif opc == 11:
+            elif opc == OPC["selb"]:
+                z = C if (scalar >> imm) & 1 else B
+            elif opc in (OPC["and"], OPC["or"], OPC["xor"]):
+                z = (A & C) if opc == OPC["and"] else (A | C) if opc == OPC["or"] else (A ^ C)
+            elif opc == OPC["st"]:
                 stored[imm] = A
                 continue
-            elif opc == 12:
-                z = C if (scalar >> imm) & 1 else B
+            elif opc == OPC["inv"]:
+                z = pow(A, P - 2, P)
+            elif opc == OPC["lin"]:
+                z = (ca * A + cb * B + cc * C + cd * D) % P
+                if (w3 >> 20) & 15 > 1:
+                    z = z * ((w3 >> 20) & 15) % P
             else:
-                x = (A - B if sb else A + B) % P
-                y = (C - D if sd else C + D) % P
-                if opc == 1:
+                x = (ca * A + cb * B) % P
+                y = (cc * C + cd * D) % P
+                if opc == OPC["muls"]:
                     z = x * y % P
-                elif opc == 2:
-                    z = x & 1           # (x * plain1) = canonical x
-                elif opc == 3:
+                elif opc == OPC["sgn0"]:
+                    z = x & 1
+                elif opc == OPC["lex"]:
                     z = 1 if x > HALF_P else 0
-                elif opc == 4:
-                    z = (x - y if sy else x + y) % P
-                elif opc == 6:
+                elif opc == OPC["eq"]:
                     z = 1 if x == y else 0
                 else:
                     raise ValueError(opc)

@@ -8,6 +8,8 @@
 
 #include "../../consensus_overlord_amd/csrc/fpvm.hpp"
 
+namespace ovh { namespace vm { constexpr uint32_t ABSENT = CONST_BASE; } }
+
 using namespace ovh;
 
 #define CHECK(x)                                                                   \
@@ -30,7 +32,7 @@ __global__ __launch_bounds__(64) void k_vm(const uint4* code, uint32_t nph, uint
   uint32_t* slots = lds + 48 + slice * NSLOT * 12;
   for (int k = 0; k < 12; ++k) slots[lane * 12 + k] = (k == 0) ? (lane + 3) : (k < 11 ? 0x1234567u * (lane + k) : 0);
   __syncthreads();
-  vm::run(code, nph, W, lane, true, slots, cst, 0);
+  vm::run(code, nph, W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
   if (lane == 0) out[blockIdx.x * 64 + threadIdx.x] = slots[0];
 }
 
@@ -44,7 +46,7 @@ __global__ __launch_bounds__(64) void k_chain(uint32_t iters, uint32_t* out) {
   out[blockIdx.x * 64 + threadIdx.x] = x.v[0];
 }
 
-static uint32_t w0(uint32_t op, uint32_t dst) { return op | dst << 8; }
+static uint32_t w0(uint32_t op, uint32_t dst) { return op | dst << 5; }
 
 int main() {
   const uint32_t NPH = 2048;
@@ -56,9 +58,9 @@ int main() {
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  const char* names[] = {"nop", "lin", "muls", "muls_half_lanes"};
+  const char* names[] = {"nop", "lin", "muls", "muls_half_lanes", "lin_coef", "muls_preadd"};
   for (uint32_t W : {16u, 64u}) {
-    for (int kind = 0; kind < 4; ++kind) {
+    for (int kind = 0; kind < 6; ++kind) {
       std::vector<uint32_t> code((size_t)(NPH + 1) * W * 4, 0);
       for (uint32_t ph = 0; ph < NPH; ++ph)
         for (uint32_t l = 0; l < W; ++l) {
@@ -68,10 +70,22 @@ int main() {
             c[0] = w0(vm::OP_LIN, l);
             c[1] = l | src << 16;
             c[2] = vm::ABSENT | vm::ABSENT << 16;
-          } else if (kind >= 2 && (kind == 2 || l % 2 == 0)) {
+            c[3] = 1 | 1 << 5;
+          } else if (kind == 4) {
+            c[0] = w0(vm::OP_LIN, l);
+            c[1] = l | src << 16;
+            c[2] = ((l + 2) % W) | ((l + 3) % W) << 16;
+            c[3] = 3 | (32 - 2) << 5 | 6 << 10 | (32 - 1) << 15;  // 3a - 2b + 6c - d
+          } else if (kind == 5) {
+            c[0] = w0(vm::OP_MULS, l);
+            c[1] = l | src << 16;
+            c[2] = ((l + 2) % W) | ((l + 3) % W) << 16;
+            c[3] = 1 | 1 << 5 | 1 << 10 | (32 - 1) << 15;  // (a + b)(c - d)
+          } else if (kind >= 2 && kind <= 3 && (kind == 2 || l % 2 == 0)) {
             c[0] = w0(vm::OP_MULS, l);
             c[1] = l | vm::ABSENT << 16;
             c[2] = src | vm::ABSENT << 16;
+            c[3] = 1 | 1 << 10;
           }
         }
       uint4* d_code;
