@@ -30,6 +30,9 @@ SIGNATURES = [
     ("ovh_batch_partial_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     ("ovh_combine_partials_device", ctypes.c_int, [_vp, _sz, _vp]),
     ("ovh_batch_fallback_device", ctypes.c_int, [_vp, _sz, _vp]),
+    ("ovh_verify_batch_device_async", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+    ("ovh_batch_wait", ctypes.c_int, [_vp]),
+    ("ovh_combine_partials_device_async", ctypes.c_int, [_vp, _sz, _vp, _sz, _vp]),
     ("ovh_stage_times", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_float), _sz]),
     ("ovh_stage_name", ctypes.c_char_p, [ctypes.c_int]),
     ("ovh_vm_trace", ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), _sz]),

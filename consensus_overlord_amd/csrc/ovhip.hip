@@ -96,6 +96,8 @@ enum : uint32_t {
 };
 // partial = (F: 12 planes, S: 6 planes)
 constexpr uint32_t PART_PLANES = 18;
+// words per fin region: 16 unpacked + 4 folded partials as planes
+constexpr size_t FIN_STRIDE = (size_t)PART_PLANES * 12 * 20;
 
 enum : int { ST_H2F = 0, ST_VOTE, ST_FOLD, ST_FINAL, ST_FALLBACK };
 static_assert(ST_FALLBACK + 1 == OVH_NSTAGES, "stage table");
@@ -186,6 +188,7 @@ __device__ __forceinline__ uint32_t slot_flag_get(const uint32_t* slots, uint32_
 __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
                                                 const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
                                                 Slab s, uint64_t seed, int32_t* __restrict__ codes) {
+  __builtin_amdgcn_s_setprio(2);  // per-vote stages outrank a co-resident final-stream wave
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -251,6 +254,7 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, const ui
 // Level 0 (codes != nullptr) takes the identity for every vote whose code is not 0.
 __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
                                                 Slab inS, Slab out, const int32_t* __restrict__ codes) {
+  __builtin_amdgcn_s_setprio(2);  // per-vote stages outrank a co-resident final-stream wave
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -317,7 +321,8 @@ __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const u
 
 // Per-vote fallback: codes[i] (still 0) := e(pk, H) == e(G1, sigma) ? 0 : VERIFY_FAIL.
 __global__ __launch_bounds__(64) void k_vm_pairchk(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g, Slab s,
-                                                   int32_t* __restrict__ codes) {
+                                                   int32_t* __restrict__ codes, const int32_t* __restrict__ verdict) {
+  if (verdict && *verdict == 1) return;  // pipelined path: the combined check passed
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -336,6 +341,22 @@ __global__ __launch_bounds__(64) void k_vm_pairchk(uint32_t n, VmDev prog, const
   vm::run(prog.code, VM_PAIRCHK_NPHASES, VM_PAIRCHK_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0},
           blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) codes[i] = slot_flag_get(slots, VM_PAIRCHK_OUT[0]) ? 0 : BLST_VERIFY_FAIL;
+}
+
+// the <= 4 fold outputs (F planes 0..11, S planes 0..5) -> a private plane set (cap 4) that the
+// final stream reads while the next batch reuses the fold scratch
+__global__ __launch_bounds__(64) void k_copy_parts(uint32_t m, Slab F, Slab S, Slab oF, Slab oS) {
+  for (uint32_t t = threadIdx.x; t < m * PART_PLANES; t += 64) {
+    const uint32_t q = t / PART_PLANES, j = t % PART_PLANES;
+    Fp v;
+    if (j < 12) {
+      F.ld(v, j, q);
+      oF.st(v, j, q);
+    } else {
+      S.ld(v, j - 12, q);
+      oS.st(v, j - 12, q);
+    }
+  }
 }
 
 // AoS partials (216 words: F 144, S 72) -> planes
@@ -509,6 +530,15 @@ struct ovh_ctx {
   int device = 0;
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
+  // pipelined batches (ovh_verify_batch_device_async): the final check + fallback of batch k run
+  // on fstream while batch k + 1's per-vote stages run on stream; two slots of batch state.
+  hipStream_t fstream = nullptr;
+  hipEvent_t ev_front[2] = {}, ev_back[2] = {};
+  uint32_t* state_slot[2] = {};
+  uint32_t* red_slot[2] = {};
+  uint32_t* fin = nullptr;       // 4 x FIN_STRIDE words: per slot, the final's partials; combine scratch
+  uint32_t pipe_k = 0;
+  int last_slot = 0;
   XmdTemplates xmd;
   std::mutex mu;  // Crypto is Send + Sync: serialise device use per context
   // batch buffers
@@ -602,12 +632,13 @@ static int vm_init(ovh_ctx* c) {
 struct StageScope {
   ovh_ctx* c;
   int k;
-  StageScope(ovh_ctx* c_, int k_) : c(c_), k(k_) {
-    if (c->flags & OVH_FLAG_PROFILE) (void)hipEventRecord(c->ev0[k], c->stream);
+  hipStream_t st;
+  StageScope(ovh_ctx* c_, int k_, hipStream_t st_ = nullptr) : c(c_), k(k_), st(st_ ? st_ : c_->stream) {
+    if (c->flags & OVH_FLAG_PROFILE) (void)hipEventRecord(c->ev0[k], st);
   }
   ~StageScope() {
     if (c->flags & OVH_FLAG_PROFILE) {
-      (void)hipEventRecord(c->ev1[k], c->stream);
+      (void)hipEventRecord(c->ev1[k], st);
       c->ev_mask |= 1u << k;
     }
   }
@@ -623,20 +654,46 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
   if (n <= c->cap && c->state) return 0;
   uint32_t cap = 256;
   while (cap < n) cap <<= 1;
-  if (c->state) (void)hipFree(c->state);
-  if (c->red) (void)hipFree(c->red);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->fstream) HIPCHK(hipStreamSynchronize(c->fstream));
+  for (int k = 0; k < 2; ++k) {
+    if (c->state_slot[k]) (void)hipFree(c->state_slot[k]);
+    if (c->red_slot[k]) (void)hipFree(c->red_slot[k]);
+    c->state_slot[k] = c->red_slot[k] = nullptr;
+  }
   if (c->st_pk) (void)hipFree(c->st_pk);
   if (c->st_sig) (void)hipFree(c->st_sig);
   if (c->codes) (void)hipFree(c->codes);
   c->state = nullptr;
   c->red = nullptr;
-  HIPCHK(hipMalloc(&c->state, (size_t)S_TOTAL * 12 * cap * 4));
   c->red_cap = cap / 4 > 64 ? cap / 4 : 64;
-  HIPCHK(hipMalloc(&c->red, (size_t)2 * PART_PLANES * 12 * c->red_cap * 4));
+  for (int k = 0; k < 2; ++k) {
+    HIPCHK(hipMalloc(&c->state_slot[k], (size_t)S_TOTAL * 12 * cap * 4));
+    HIPCHK(hipMalloc(&c->red_slot[k], (size_t)2 * PART_PLANES * 12 * c->red_cap * 4));
+  }
+  c->state = c->state_slot[0];
+  c->red = c->red_slot[0];
   HIPCHK(hipMalloc(&c->st_pk, (size_t)cap * 4));
   HIPCHK(hipMalloc(&c->st_sig, (size_t)cap * 4));
   HIPCHK(hipMalloc(&c->codes, (size_t)cap * 4));
   c->cap = cap;
+  return 0;
+}
+
+// Wait for pipelined batch work on the final stream (APIs that reuse the batch state as
+// scratch call this first).
+static int drain(ovh_ctx* c) {
+  if (c->fstream) HIPCHK(hipStreamSynchronize(c->fstream));
+  return 0;
+}
+
+// Batch state slot k for the next batch on the main stream: the stream first waits until the
+// final stream has finished with the slot's previous batch (its fallback reads that state).
+static int take_slot(ovh_ctx* c, int k) {
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_back[k], 0));
+  c->state = c->state_slot[k];
+  c->red = c->red_slot[k];
+  c->last_slot = k;
   return 0;
 }
 
@@ -673,6 +730,21 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
     ovh_destroy(c);
     return nullptr;
   }
+  {
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
+    if (hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) != hipSuccess ||
+        hipMalloc(&c->fin, (size_t)4 * FIN_STRIDE * 4) != hipSuccess) {
+      ovh_destroy(c);
+      return nullptr;
+    }
+    for (int k = 0; k < 2; ++k)
+      if (hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c->ev_back[k], hipEventDisableTiming) != hipSuccess) {
+        ovh_destroy(c);
+        return nullptr;
+      }
+  }
   if (flags & OVH_FLAG_PROFILE)
     for (int k = 0; k < OVH_NSTAGES; ++k)
       if (hipEventCreate(&c->ev0[k]) != hipSuccess || hipEventCreate(&c->ev1[k]) != hipSuccess) {
@@ -686,9 +758,16 @@ void ovh_destroy(ovh_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (void* p : {(void*)c->state, (void*)c->red, (void*)c->st_pk, (void*)c->st_sig, (void*)c->codes,
-                  (void*)c->in_buf, (void*)c->partial, (void*)c->result, (void*)c->vm_consts})
+  if (c->fstream) (void)hipStreamSynchronize(c->fstream);
+  for (void* p : {(void*)c->state_slot[0], (void*)c->state_slot[1], (void*)c->red_slot[0], (void*)c->red_slot[1],
+                  (void*)c->st_pk, (void*)c->st_sig, (void*)c->codes, (void*)c->in_buf, (void*)c->partial,
+                  (void*)c->result, (void*)c->vm_consts, (void*)c->fin})
     if (p) (void)hipFree(p);
+  if (c->fstream) (void)hipStreamDestroy(c->fstream);
+  for (int k = 0; k < 2; ++k) {
+    if (c->ev_front[k]) (void)hipEventDestroy(c->ev_front[k]);
+    if (c->ev_back[k]) (void)hipEventDestroy(c->ev_back[k]);
+  }
   for (void* p : c->vm_bufs) (void)hipFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (int k = 0; k < OVH_NSTAGES; ++k) {
@@ -832,7 +911,7 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
   if (n && (!sig_lens || !pk_lens)) return OVH_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  if (ensure_cap(c, n > 0 ? n : 1)) return OVH_ERR_DEVICE;
+  if (drain(c) || ensure_cap(c, n > 0 ? n : 1)) return OVH_ERR_DEVICE;
   // the staging buffer may be reallocated by the second stage_list: stage both first, then launch
   uint8_t *ds, *dp;
   uint64_t *so, *sl, *po, *pl;
@@ -881,7 +960,7 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
 // Parses + sums a pk list on the device; the Jacobian sum (36 words) stays at *d_sum.
 static int sum_pks(ovh_ctx* c, const uint8_t* pks, const size_t* pk_lens, size_t n, uint8_t* out48, uint32_t** d_sum) {
   if (n && !pk_lens) return OVH_ERR_ARG;
-  if (ensure_cap(c, n > 0 ? n : 1)) return OVH_ERR_DEVICE;
+  if (drain(c) || ensure_cap(c, n > 0 ? n : 1)) return OVH_ERR_DEVICE;
   size_t t = 0;
   for (size_t i = 0; i < n; ++i) t += pk_lens[i];
   if (ensure_in(c, t + 16 * (n + 1) + 256)) return OVH_ERR_DEVICE;
@@ -989,6 +1068,10 @@ static int batch_front(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint
   return 0;
 }
 
+// Verdict words in c->result: [0] single-call APIs, [8 + slot] pipelined batches,
+// [10 + slot] pipelined combines, [12] synchronous combine.
+enum { RES_BATCH = 8, RES_COMBINE = 10, RES_SYNC = 12 };
+
 int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
                              uint64_t seed, int32_t* d_codes, uint8_t* d_partial) {
   if (!c || !d_codes || !d_partial || (n && (!d_sigs || !d_hashes || !d_pks))) return OVH_ERR_ARG;
@@ -1001,9 +1084,11 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
     for (int k = 0; k < 12; ++k) p[144 + 24 + k] = ONE_M[k];  // Y.c0 = 1
     HIPCHK(hipMemcpyAsync(d_partial, p.data(), 864, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    c->last_n = 0;
     return 0;
   }
   if (ensure_cap(c, n)) return OVH_ERR_DEVICE;
+  if (take_slot(c, (int)(c->pipe_k++ & 1))) return OVH_ERR_DEVICE;
   Slab F, S;
   uint32_t m;
   int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m);
@@ -1022,16 +1107,41 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   return 0;
 }
 
-// Combined check on <= 4 partials given as planes (fold further if needed by the caller).
-static int final_check(ovh_ctx* c, Slab F, Slab S, uint32_t m, int32_t* r_host) {
-  {
-    StageScope p(c, ST_FINAL);
-    k_vm_final<<<1, 64, LDS_FINAL, c->stream>>>(m, c->vm_final, c->vm_consts, F, S, c->result);
+// Final check on <= 4 partials given as planes: k_vm_final on stream `st`, verdict to *d_res.
+static void enqueue_final(ovh_ctx* c, hipStream_t st, Slab F, Slab S, uint32_t m, int32_t* d_res) {
+  StageScope p(c, ST_FINAL, st);
+  k_vm_final<<<1, 64, LDS_FINAL, st>>>(m, c->vm_final, c->vm_consts, F, S, d_res);
+}
+
+// Per-vote fallback of the batch in state slot `slot`, on stream `st`, skipped on the device
+// when *d_verdict == 1 (d_verdict null: always runs).
+static void enqueue_fallback(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, int32_t* d_codes,
+                             const int32_t* d_verdict) {
+  StageScope p(c, ST_FALLBACK, st);
+  k_vm_pairchk<<<(n + VM_SLICES - 1) / VM_SLICES, 64, LDS_PAIRCHK, st>>>(
+      n, c->vm_pairchk, c->vm_consts, Slab{c->state_slot[slot], c->cap}, d_codes, d_verdict);
+}
+
+// AoS partials (k <= 16) -> <= 4 partials as planes in the fin area of `slot` (unpack, and one
+// fold level when k > 4), on stream st. Scratch: fin slot area + the slot's upper half.
+static int stage_partials(ovh_ctx* c, hipStream_t st, size_t k, const uint8_t* d_partials, uint32_t* scratch,
+                          Slab* F, Slab* S, uint32_t* m) {
+  Slab uF{scratch, 16}, uS{scratch + (size_t)12 * 12 * 16, 16};
+  k_unpack_partials<<<(uint32_t)((k * PART_PLANES + 63) / 64), 64, 0, st>>>((uint32_t)k, (const uint32_t*)d_partials,
+                                                                           uF, uS);
+  if (k <= 4) {
+    *F = uF;
+    *S = uS;
+    *m = (uint32_t)k;
+  } else {
+    uint32_t* o = scratch + (size_t)PART_PLANES * 12 * 16;
+    Slab oF{o, 4};
+    k_vm_fold<<<1, 64, LDS_FOLD, st>>>((uint32_t)k, c->vm_fold, c->vm_consts, uF, uS, oF, nullptr);
+    *F = oF;
+    *S = Slab{o + (size_t)12 * 12 * 4, 4};
+    *m = (uint32_t)((k + 3) / 4);
   }
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(r_host, c->result, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return 0;
+  return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
 }
 
 int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials) {
@@ -1039,8 +1149,8 @@ int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials)
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return -OVH_ERR_DEVICE;
   if (ensure_cap(c, k * 4 > 256 ? k * 4 : 256)) return -OVH_ERR_DEVICE;
-  // AoS partials -> planes in the state slab (F at S_F, S at S_RS), then fold to <= 4
-  Slab s{c->state, c->cap};
+  if (drain(c)) return -OVH_ERR_DEVICE;
+  // AoS partials -> planes (F at S_F, S at S_RS of the current slot's state), fold to <= 4
   Slab F{c->state + (size_t)S_F * 12 * c->cap, c->cap}, S{c->state + (size_t)S_RS * 12 * c->cap, c->cap};
   k_unpack_partials<<<(uint32_t)((k * PART_PLANES + 63) / 64), 64, 0, c->stream>>>((uint32_t)k,
                                                                                    (const uint32_t*)d_partials, F, S);
@@ -1057,10 +1167,12 @@ int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials)
     m = mo;
     flip ^= 1;
   }
-  (void)s;
+  enqueue_final(c, c->stream, F, S, m, c->result + RES_SYNC);
   if (hipGetLastError() != hipSuccess) return -OVH_ERR_DEVICE;
   int32_t r = -1;
-  if (final_check(c, F, S, m, &r)) return -OVH_ERR_DEVICE;
+  if (hipMemcpyAsync(&r, c->result + RES_SYNC, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return -OVH_ERR_DEVICE;
   return r;
 }
 
@@ -1070,41 +1182,72 @@ int ovh_batch_fallback_device(ovh_ctx* c, size_t n, int32_t* d_codes) {
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return 0;
   if (n != c->last_n) return OVH_ERR_ARG;
-  Slab s{c->state, c->cap};
-  {
-    StageScope p(c, ST_FALLBACK);
-    k_vm_pairchk<<<(uint32_t)((n + VM_SLICES - 1) / VM_SLICES), 64, LDS_PAIRCHK, c->stream>>>(
-        (uint32_t)n, c->vm_pairchk, c->vm_consts, s, d_codes);
-  }
+  enqueue_fallback(c, c->stream, c->last_slot, (uint32_t)n, d_codes, nullptr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
 
-int ovh_verify_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
-                            uint64_t seed, int32_t* d_codes) {
+int ovh_combine_partials_device_async(ovh_ctx* c, size_t k, const uint8_t* d_partials, size_t n, int32_t* d_codes) {
+  if (!c || !d_partials || k == 0 || k > 16 || (n && !d_codes)) return OVH_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  if (n != c->last_n) return OVH_ERR_ARG;
+  const int slot = c->last_slot;
+  // the partials were produced (and gathered) before this call returned to the host
+  uint32_t* scratch = c->fin + (size_t)(2 + slot) * FIN_STRIDE;
+  Slab F, S;
+  uint32_t m;
+  if (stage_partials(c, c->fstream, k, d_partials, scratch, &F, &S, &m)) return OVH_ERR_DEVICE;
+  int32_t* verdict = c->result + RES_COMBINE + slot;
+  enqueue_final(c, c->fstream, F, S, m, verdict);
+  if (n) enqueue_fallback(c, c->fstream, slot, (uint32_t)n, d_codes, verdict);
+  HIPCHK(hipEventRecord(c->ev_back[slot], c->fstream));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ovh_verify_batch_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
+                                  const uint8_t* d_pks, uint64_t seed, int32_t* d_codes) {
   if (!c || (n && (!d_sigs || !d_hashes || !d_pks || !d_codes))) return OVH_ERR_ARG;
   if (n == 0) return 0;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   if (ensure_cap(c, n)) return OVH_ERR_DEVICE;
+  const int slot = (int)(c->pipe_k++ & 1);
+  if (take_slot(c, slot)) return OVH_ERR_DEVICE;
   Slab F, S;
   uint32_t m;
   int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m);
   if (e) return e;
-  int32_t r = -1;
-  if (final_check(c, F, S, m, &r)) return OVH_ERR_DEVICE;
-  if (r != 1) {
-    Slab s{c->state, c->cap};
-    {
-      StageScope p(c, ST_FALLBACK);
-      k_vm_pairchk<<<(uint32_t)((n + VM_SLICES - 1) / VM_SLICES), 64, LDS_PAIRCHK, c->stream>>>(
-          (uint32_t)n, c->vm_pairchk, c->vm_consts, s, d_codes);
-    }
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(c->stream));
-  }
+  // hand the <= 4 fold outputs to the final stream through the slot's private copy
+  uint32_t* fb = c->fin + (size_t)slot * FIN_STRIDE;
+  Slab oF{fb, 4}, oS{fb + (size_t)12 * 12 * 4, 4};
+  k_copy_parts<<<1, 64, 0, c->stream>>>(m, F, S, oF, oS);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
+  HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_front[slot], 0));
+  int32_t* verdict = c->result + RES_BATCH + slot;
+  enqueue_final(c, c->fstream, oF, oS, m, verdict);
+  enqueue_fallback(c, c->fstream, slot, (uint32_t)n, d_codes, verdict);
+  HIPCHK(hipEventRecord(c->ev_back[slot], c->fstream));
+  HIPCHK(hipGetLastError());
   return 0;
+}
+
+int ovh_batch_wait(ovh_ctx* c) {
+  if (!c) return OVH_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipStreamSynchronize(c->fstream));
+  return 0;
+}
+
+int ovh_verify_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
+                            uint64_t seed, int32_t* d_codes) {
+  int e = ovh_verify_batch_device_async(c, n, d_sigs, d_hashes, d_pks, seed, d_codes);
+  return e ? e : ovh_batch_wait(c);
 }
 
 int ovh_verify_batch(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks, uint64_t seed,

@@ -60,3 +60,22 @@ def combine_partials(ctx: Context, partials: torch.Tensor) -> bool:
 
 def batch_fallback(ctx: Context, n: int, codes: torch.Tensor) -> None:
     raise_for(ctx.lib.ovh_batch_fallback_device(ctx.ptr, n, _ptr(codes)))
+
+
+def verify_batch_async(ctx: Context, sigs: torch.Tensor, hashes: torch.Tensor, pks: torch.Tensor, seed: int,
+                       codes: torch.Tensor) -> None:
+    """Enqueue one batch (ovh_verify_batch_device_async); `codes` is final after batch_wait."""
+    n = sigs.shape[0]
+    raise_for(ctx.lib.ovh_verify_batch_device_async(ctx.ptr, n, _ptr(sigs), _ptr(hashes), _ptr(pks),
+                                                    seed & 0xFFFFFFFFFFFFFFFF, _ptr(codes)))
+
+
+def combine_partials_async(ctx: Context, partials: torch.Tensor, n: int, codes: torch.Tensor) -> None:
+    """Enqueue the combined check of the gathered partials and, device-gated on its verdict,
+    the fallback of this rank's last partial's n votes into `codes` (final after batch_wait)."""
+    raise_for(ctx.lib.ovh_combine_partials_device_async(ctx.ptr, partials.shape[0], _ptr(partials), n,
+                                                        _ptr(codes)))
+
+
+def batch_wait(ctx: Context) -> None:
+    raise_for(ctx.lib.ovh_batch_wait(ctx.ptr))

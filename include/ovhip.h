@@ -106,6 +106,21 @@ int ovh_combine_partials_device(ovh_ctx* ctx, size_t k, const uint8_t* d_partial
  * exact per-vote verify result for every vote whose code is still 0. */
 int ovh_batch_fallback_device(ovh_ctx* ctx, size_t n, int32_t* d_codes);
 
+/* Pipelined batches. ovh_verify_batch_device_async enqueues one batch and returns without
+ * waiting: the per-vote stages run on ovh_stream, the combined check and (device-gated) per-vote
+ * fallback on a second, lower-priority stream, so batch k's final exponentiation overlaps batch
+ * k + 1's per-vote work. Two batches may be in flight per context; d_codes of a batch must stay
+ * untouched until ovh_batch_wait returns, after which they hold exactly the per-vote
+ * ovh_verify results. ovh_verify_batch_device = the async call + ovh_batch_wait. */
+int ovh_verify_batch_device_async(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
+                                  const uint8_t* d_pks, uint64_t seed, int32_t* d_codes);
+int ovh_batch_wait(ovh_ctx* ctx);
+/* Multi-GPU form: after ovh_batch_partial_device (n votes of this rank) and the all-gather of
+ * the k <= 16 partials, enqueue the combined check and, if it fails, the per-vote fallback of
+ * this rank's n votes into d_codes, on the second stream; ovh_batch_wait completes it. */
+int ovh_combine_partials_device_async(ovh_ctx* ctx, size_t k, const uint8_t* d_partials, size_t n,
+                                      int32_t* d_codes);
+
 /* Device time (ms, HIP events on ovh_stream) of each stage of the most recent batch call
  * (ovh_verify_batch_device / ovh_batch_partial_device / ovh_combine_partials_device /
  * ovh_batch_fallback_device) on a context created with OVH_FLAG_PROFILE; stages that did not

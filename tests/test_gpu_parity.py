@@ -174,3 +174,59 @@ def test_partials_combine_two_shards(cc):
     dev.batch_partial(cc.ctx, sigs[:h], hs2[:h], pks[:h], 11, codes[:h], parts[0])
     dev.batch_partial(cc.ctx, sigs[h:], hs2[h:], pks[h:], 12, codes[h:], parts[1])
     assert not dev.combine_partials(cc.ctx, parts)
+
+
+def test_pipelined_batches_with_invalid(cc):
+    """Four batches in flight through ovh_verify_batch_device_async (two state slots): batch 1
+    holds invalid votes, so its device-gated fallback runs on the final stream while batch 2's
+    per-vote stages run; every batch's codes equal the per-vote verdicts after batch_wait."""
+    import torch
+    import bls12_381 as bls
+    from consensus_overlord_amd import device as dev
+    n = 192
+    sks, hs = _synth(n, seed=21)
+    pks = dev.sk_to_pk_batch(cc.ctx, sks)
+    sigs = dev.sign_batch(cc.ctx, sks, hs)
+    s_host = sigs.cpu().numpy().copy()
+    bad = [3, 77, 150]
+    for i in bad:
+        pt = bls.g2_from_bytes(bytes(s_host[i]))
+        s_host[i] = np.frombuffer(bls.g2_compress(bls.pt_add(bls.Fp2Ops, pt, bls.G2_GEN)), dtype=np.uint8)
+    sigs_bad = torch.from_numpy(s_host).cuda()
+    codes = torch.full((4, n), -1, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    for b, sg in enumerate((sigs, sigs_bad, sigs, sigs_bad)):
+        dev.verify_batch_async(cc.ctx, sg, hs, pks, 40 + b, codes[b])
+    dev.batch_wait(cc.ctx)
+    c = codes.cpu().numpy()
+    assert (c[0] == 0).all() and (c[2] == 0).all()
+    for b in (1, 3):
+        assert [i for i in range(n) if c[b, i] != 0] == bad
+        assert all(c[b, i] == 5 for i in bad)
+
+
+def test_pipelined_combine_async(cc):
+    """Multi-GPU form on one device: partial -> combine_partials_async (final stream, fallback
+    gated on the verdict) for a valid and an invalid shard pair."""
+    import torch
+    from consensus_overlord_amd import device as dev
+    n = 96
+    sks, hs = _synth(n, seed=33)
+    pks = dev.sk_to_pk_batch(cc.ctx, sks)
+    sigs = dev.sign_batch(cc.ctx, sks, hs)
+    h = n // 2
+    hs2 = hs.clone()
+    hs2[[1, 2]] = hs[[2, 1]]       # two votes of shard 0 sign the other's digest
+    torch.cuda.synchronize()
+    out = []
+    for hh in (hs, hs2):
+        parts = torch.empty((2, 864), dtype=torch.uint8, device="cuda")
+        c1 = torch.full((h,), -1, dtype=torch.int32, device="cuda")
+        c0 = torch.full((h,), -1, dtype=torch.int32, device="cuda")
+        dev.batch_partial(cc.ctx, sigs[h:], hh[h:], pks[h:], 5, c1, parts[1])
+        dev.batch_partial(cc.ctx, sigs[:h], hh[:h], pks[:h], 6, c0, parts[0])
+        dev.combine_partials_async(cc.ctx, parts, h, c0)   # fallback for the last partial's shard
+        dev.batch_wait(cc.ctx)
+        out.append(c0.cpu().numpy())
+    assert (out[0] == 0).all()
+    assert [i for i in range(h) if out[1][i] != 0] == [1, 2] and all(out[1][i] == 5 for i in (1, 2))
