@@ -121,6 +121,7 @@ def main():
     import torch.distributed as dist
     from consensus_overlord_amd import device as dev
     from consensus_overlord_amd.crypto import Context
+    from consensus_overlord_amd.shard import DeviceBackend, ShardVerifier
 
     torch.cuda.set_device(local)
     if world > 1:
@@ -137,7 +138,7 @@ def main():
     sigs = dev.sign_batch(ctx, sks, hs)
     nbatch = args.warmup + args.steps + args.profile_steps
     codes = torch.full((nbatch, B), -1, dtype=torch.int32, device="cuda")   # one verdict row per batch
-    partials = torch.empty((2, world, 864), dtype=torch.uint8, device="cuda")
+    shards = ShardVerifier(DeviceBackend(ctx)) if world > 1 else None
     torch.cuda.synchronize()
 
     nst = NSTAGES
@@ -145,21 +146,24 @@ def main():
     stage_ms = np.zeros(nst)
     buf = (ctypes.c_float * nst)()
 
+    def wait_all() -> None:
+        if shards:
+            shards.wait()
+        else:
+            dev.batch_wait(ctx)
+
     def step(s: int) -> None:
         """Enqueue batch s. Pipelined: batch s's combined check / fallback (second stream) overlaps
         batch s + 1's per-vote stages; every batch's codes row is final after batch_wait."""
-        seed = (SEED << 32) ^ (s * 0x10001 + rank)
+        seed = (SEED << 32) ^ (s * 0x10001)
         if world == 1:
             dev.verify_batch_async(ctx, sigs, hs, pks, seed, codes[s])
         else:
-            part = partials[s % 2]
-            dev.batch_partial(ctx, sigs, hs, pks, seed, codes[s], part[rank])
-            dist.all_gather_into_tensor(part, part[rank].clone())
-            dev.combine_partials_async(ctx, part, B, codes[s])
+            shards.submit(s, sigs, hs, pks, seed, codes[s])
 
     for s in range(args.warmup):
         step(s)
-    dev.batch_wait(ctx)
+    wait_all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -167,7 +171,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         step(args.warmup + s)
-    dev.batch_wait(ctx)
+    wait_all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -185,7 +189,7 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         step(s)
-        dev.batch_wait(ctx)
+        wait_all()
         lat.append(time.perf_counter() - t1)
         got = lib.ovh_stage_times(ctx.ptr, buf, nst)
         if got != nst:

@@ -1,0 +1,79 @@
+"""Multi-GPU batch verification: one process per GPU, each rank verifies its
+own shard of votes -- weak scaling, the votes are independent units -- and the only data
+exchange per batch is an all-gather of the 864-byte per-shard partials (Fp12 Miller product +
+projective G2 sum, include/ovhip.h OVH_PARTIAL_BYTES): RCCL over xGMI between GPUs, gloo on
+CPU. Every rank then runs the same combined check on the gathered partials and, only if it
+fails, the per-vote fallback of its own shard, so each rank ends with the exact per-vote codes
+of its votes (ConsensusCrypto::verify_signature, src/consensus.rs:397-416, vote by vote).
+
+Batches are pipelined: batch s's combined check / fallback is enqueued on the backend's second
+stream and overlaps batch s + 1's per-vote stages; `wait()` completes everything submitted.
+
+The backend supplies the compute (DeviceBackend = libovhip on this rank's GPU; the CPU tests
+plug in the C oracle); this module is the orchestration both share.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+PARTIAL_BYTES = 864
+
+
+class DeviceBackend:
+    """libovhip on the current GPU (consensus_overlord_amd.device)."""
+
+    def __init__(self, ctx):
+        from . import device
+        self.ctx = ctx
+        self.dev = device
+
+    def empty_partials(self, world: int) -> torch.Tensor:
+        return torch.empty((2, world, PARTIAL_BYTES), dtype=torch.uint8, device="cuda")
+
+    def partial(self, sigs, hashes, pks, seed: int, codes, out_row) -> None:
+        self.dev.batch_partial(self.ctx, sigs, hashes, pks, seed, codes, out_row)
+
+    def combine_async(self, parts, n: int, codes) -> None:
+        self.dev.combine_partials_async(self.ctx, parts, n, codes)
+
+    def wait(self) -> None:
+        self.dev.batch_wait(self.ctx)
+
+
+class ShardVerifier:
+    """Per-rank driver: submit(s, ...) verifies this rank's shard of batch s."""
+
+    def __init__(self, backend, group=None):
+        self.backend = backend
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.nccl = dist.get_backend(group) == "nccl"
+        self.partials = backend.empty_partials(self.world)   # two in flight (pipelining)
+
+    def _all_gather(self, part: torch.Tensor) -> None:
+        mine = part[self.rank].clone()
+        if self.nccl:
+            dist.all_gather_into_tensor(part, mine, group=self.group)
+        else:
+            dist.all_gather(list(part.unbind(0)), mine, group=self.group)
+
+    def submit(self, s: int, sigs, hashes, pks, seed: int, codes) -> None:
+        """Enqueue batch s: this rank's n votes -> partial -> all-gather -> combined check and
+        (device-gated) fallback into `codes`, final after wait()."""
+        part = self.partials[s % 2]
+        seed = (seed ^ (self.rank * 0x9E3779B97F4A7C15)) & 0xFFFFFFFFFFFFFFFF   # rank-distinct RLC scalars
+        self.backend.partial(sigs, hashes, pks, seed, codes, part[self.rank])
+        self._all_gather(part)
+        self.backend.combine_async(part, sigs.shape[0], codes)
+
+    def wait(self) -> None:
+        self.backend.wait()
+
+
+def shard_bounds(n_total: int, world: int, rank: int):
+    """Contiguous shard [lo, hi) of rank `rank` when n_total votes are split over `world` ranks."""
+    base, extra = divmod(n_total, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)

@@ -1579,6 +1579,106 @@ int orc_verify_batch_rlc(size_t n, const uint8_t* sigs, const uint8_t* hashes, c
   return OK;
 }
 
+/* ---- multi-GPU split of orc_verify_batch_rlc in libovhip's partial format ----
+ * (include/ovhip.h, OVH_PARTIAL_BYTES = 864): F (576 B) = Fp12 product of the shard's Miller
+ * outputs as 12 Fp in Montgomery form (R = 2^384, little-endian limbs), c0.c0.c0 first -- the
+ * fp12 struct's own layout; S (288 B) = sum of r_i sig_i in homogeneous projective
+ * coordinates (X : Y : Z), O = (0 : 1 : 0). Partials from this oracle and from the GPU combine
+ * with each other: they differ only by line scalings the final exponentiation removes. */
+static void part_write(uint8_t* out, const fp12* f, const g2_jac* S) {
+  fp2 X, Y, Z, z2;
+  memcpy(out, f, 576);
+  if (f2_is_zero(&S->Z)) {
+    memset(&X, 0, sizeof X);
+    f2_one(&Y);
+    memset(&Z, 0, sizeof Z);
+  } else { /* Jacobian (x = X / Z^2, y = Y / Z^3) -> homogeneous (X Z : Y : Z^3) */
+    f2_mul(&X, &S->X, &S->Z);
+    Y = S->Y;
+    f2_sqr(&z2, &S->Z);
+    f2_mul(&Z, &z2, &S->Z);
+  }
+  memcpy(out + 576, &X, 96);
+  memcpy(out + 672, &Y, 96);
+  memcpy(out + 768, &Z, 96);
+}
+
+static void part_read(fp12* f, g2_jac* S, const uint8_t* in) {
+  fp2 X, Y, Z, z2;
+  memcpy(f, in, 576);
+  memcpy(&X, in + 576, 96);
+  memcpy(&Y, in + 672, 96);
+  memcpy(&Z, in + 768, 96);
+  if (f2_is_zero(&Z)) {
+    g2_set_inf(S);
+    return;
+  } /* homogeneous -> Jacobian (X Z : Y Z^2 : Z) */
+  f2_mul(&S->X, &X, &Z);
+  f2_sqr(&z2, &Z);
+  f2_mul(&S->Y, &Y, &z2);
+  S->Z = Z;
+}
+
+/* Per-shard partial of the RLC batch (codes[i] = parse / subgroup codes, OK for the votes
+ * that entered the partial); out864 as above. */
+int orc_batch_partial(size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks, uint64_t seed,
+                      int32_t* codes, int threads, uint8_t* out864) {
+  init();
+  if (threads < 1) threads = 1;
+  fp12 f;
+  g2_jac S;
+  f12_one(&f);
+  g2_set_inf(&S);
+  if (n) {
+    job_t* jobs = make_jobs(n, threads, sigs, hashes, pks, codes, seed);
+    if (!jobs) return ERR_ARG;
+    run_jobs(jobs, threads, rlc_worker);
+    for (int t = 0; t < threads; ++t) {
+      f12_mul(&f, &f, &jobs[t].f);
+      g2_add(&S, &S, &jobs[t].S);
+    }
+    free(jobs);
+  }
+  part_write(out864, &f, &S);
+  return OK;
+}
+
+/* Combined check of k partials: *ok = [prod F * Miller(-G1, sum S)]^FE == 1. */
+int orc_combine_partials(size_t k, const uint8_t* parts, int* ok) {
+  init();
+  if (!parts || !ok || k == 0) return ERR_ARG;
+  fp12 f, fi, m;
+  g2_jac S, Si;
+  f12_one(&f);
+  g2_set_inf(&S);
+  for (size_t i = 0; i < k; ++i) {
+    part_read(&fi, &Si, parts + 864 * i);
+    f12_mul(&f, &f, &fi);
+    g2_add(&S, &S, &Si);
+  }
+  g2_aff Sa;
+  g2_to_aff(&Sa, &S);
+  miller_loop(&m, &G1_NEG_A, &Sa);
+  f12_mul(&f, &f, &m);
+  final_exp(&f, &f);
+  *ok = f12_is_one(&f);
+  return OK;
+}
+
+/* The per-vote fallback of a shard whose combined check failed: every code still OK becomes
+ * orc_verify's code. */
+int orc_batch_fallback(size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks, int32_t* codes,
+                       int threads) {
+  init();
+  if (threads < 1) threads = 1;
+  if (!n) return OK;
+  job_t* jobs = make_jobs(n, threads, sigs, hashes, pks, codes, 0);
+  if (!jobs) return ERR_ARG;
+  run_jobs(jobs, threads, rlc_fallback_worker);
+  free(jobs);
+  return OK;
+}
+
 /* e(G1, G2)^3 coefficients (c0.c0.c0, c0.c0.c1, c0.c1.c0, ...), 12 x 48 BE bytes */
 void orc_gt_g1g2(uint8_t out576[576]) {
   init();

@@ -39,6 +39,9 @@ def load(build_if_missing: bool = True):
         "orc_verify_batch_rlc": (ctypes.c_int, [_sz, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int,
                                                 ctypes.POINTER(ctypes.c_int)]),
         "orc_gt_g1g2": (None, [_u8]),
+        "orc_batch_partial": (ctypes.c_int, [_sz, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int, _vp]),
+        "orc_combine_partials": (ctypes.c_int, [_sz, _vp, ctypes.POINTER(ctypes.c_int)]),
+        "orc_batch_fallback": (ctypes.c_int, [_sz, _vp, _vp, _vp, _vp, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -133,3 +136,33 @@ def gt_g1g2() -> list:
     out = ctypes.create_string_buffer(576)
     load().orc_gt_g1g2(out)
     return ["%096x" % int.from_bytes(out.raw[48 * i:48 * i + 48], "big") for i in range(12)]
+
+
+def batch_partial(sigs, hashes, pks, seed: int, threads: int = 1):
+    """orc_batch_partial: -> (codes, 864-byte partial in libovhip's format)."""
+    s, sp = _arr(sigs, 96)
+    h, hp = _arr(hashes, 32)
+    p, pp = _arr(pks, 48)
+    n = s.shape[0]
+    codes = np.zeros(max(n, 1), dtype=np.int32)
+    out = np.zeros(864, dtype=np.uint8)
+    assert load().orc_batch_partial(n, sp, hp, pp, seed & 0xFFFFFFFFFFFFFFFF, codes.ctypes.data_as(ctypes.c_void_p),
+                                    threads, out.ctypes.data_as(ctypes.c_void_p)) == 0
+    return codes[:n], out
+
+
+def combine_partials(parts) -> bool:
+    """orc_combine_partials over a (k, 864) uint8 array."""
+    a = np.ascontiguousarray(parts, dtype=np.uint8).reshape(-1, 864)
+    ok = ctypes.c_int(0)
+    assert load().orc_combine_partials(a.shape[0], a.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ok)) == 0
+    return bool(ok.value)
+
+
+def batch_fallback(sigs, hashes, pks, codes: np.ndarray, threads: int = 1) -> None:
+    """orc_batch_fallback: codes (int32, in place) still 0 -> the per-vote verify code."""
+    s, sp = _arr(sigs, 96)
+    h, hp = _arr(hashes, 32)
+    p, pp = _arr(pks, 48)
+    assert codes.dtype == np.int32 and codes.flags.c_contiguous
+    assert load().orc_batch_fallback(s.shape[0], sp, hp, pp, codes.ctypes.data_as(ctypes.c_void_p), threads) == 0

@@ -230,3 +230,29 @@ def test_pipelined_combine_async(cc):
         out.append(c0.cpu().numpy())
     assert (out[0] == 0).all()
     assert [i for i in range(h) if out[1][i] != 0] == [1, 2] and all(out[1][i] == 5 for i in (1, 2))
+
+
+def test_partials_interoperate_with_oracle(cc):
+    """A GPU shard partial and a C-oracle shard partial (same 864-byte format) combine on the GPU
+    and in the oracle to the same verdict: valid batch -> pass, cross-shard digest swap -> fail."""
+    import torch
+    import orc
+    from consensus_overlord_amd import device as dev
+    n = 64
+    sks, hs = _synth(n, seed=44)
+    pks = dev.sk_to_pk_batch(cc.ctx, sks)
+    sigs = dev.sign_batch(cc.ctx, sks, hs)
+    h = n // 2
+    for swap, want in ((False, True), (True, False)):
+        hh = hs.clone()
+        if swap:
+            hh[[0, h]] = hs[[h, 0]]
+        torch.cuda.synchronize()
+        parts = torch.empty((2, 864), dtype=torch.uint8, device="cuda")
+        codes = torch.empty((h,), dtype=torch.int32, device="cuda")
+        dev.batch_partial(cc.ctx, sigs[:h], hh[:h], pks[:h], 71, codes, parts[0])
+        c1, p1 = orc.batch_partial(sigs[h:].cpu().numpy(), hh[h:].cpu().numpy(), pks[h:].cpu().numpy(), 72)
+        assert (c1 == 0).all()
+        parts[1] = torch.from_numpy(p1).cuda()
+        assert dev.combine_partials(cc.ctx, parts) == want
+        assert orc.combine_partials(parts.cpu().numpy()) == want
