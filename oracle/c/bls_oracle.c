@@ -1525,14 +1525,22 @@ static void* rlc_worker(void* arg) {
       continue;
     }
     j->codes[i] = OK;
+    /* r = a + b lambda (mod r), lambda = -x^2, (a, b) = the 32-bit halves of SplitMix64 (the
+     * device's tools/fpvm/alg.py LAMBDA): [r] pk = [a] pk + [b] phi(pk), [r] sig = [a] sig +
+     * [b] (-psi^2(sig)); pk in G1 and sig in G2 were checked above. */
     const uint64_t r = splitmix(j->seed, i);
-    g1_jac rp;
-    g1_mul_words(&rp, &pj, &r, 1);
+    const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
+    g1_jac rp, phi = pj;
+    fp_mul(&phi.X, &pj.X, &BETA);
+    g1_mul2_32(&rp, &pj, &phi, ra, rb);
     g1_aff rpa;
     g1_to_aff(&rpa, &rp);
-    g2_jac sj, rs;
+    g2_jac sj, rs, ps;
     g2_from_aff(&sj, &s);
-    g2_mul_words(&rs, &sj, &r, 1);
+    g2_psi(&ps, &sj);
+    g2_psi(&ps, &ps);
+    g2_neg(&ps, &ps);
+    g2_mul2_32(&rs, &sj, &ps, ra, rb);
     g2_add(&j->S, &j->S, &rs);
     fp12 m;
     miller_loop(&m, &rpa, &h);

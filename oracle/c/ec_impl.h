@@ -160,6 +160,21 @@ static void PT_(mul_words)(PT_(jac) * r, const PT_(jac) * p, const uint64_t* k, 
   *r = acc;
 }
 
+/* [a] p + [b] q for 32-bit a, b (public): one shared double-and-add chain (Shamir) */
+static void PT_(mul2_32)(PT_(jac) * r, const PT_(jac) * p, const PT_(jac) * q, uint32_t a, uint32_t b) {
+  PT_(jac) pq, acc;
+  PT_(add)(&pq, p, q);
+  PT_(set_inf)(&acc);
+  for (int k = 31; k >= 0; --k) {
+    PT_(dbl)(&acc, &acc);
+    const int ba = (a >> k) & 1, bb = (b >> k) & 1;
+    if (ba && bb) PT_(add)(&acc, &acc, &pq);
+    else if (ba) PT_(add)(&acc, &acc, p);
+    else if (bb) PT_(add)(&acc, &acc, q);
+  }
+  *r = acc;
+}
+
 static int PT_(on_curve)(const PT_(aff) * a) {
   if (a->inf) return 1;
   FT l, rr, t;

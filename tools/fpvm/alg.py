@@ -23,6 +23,19 @@ import sys
 from ir import P, Prog
 
 X_ABS = 0xD201000000010000
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+# RLC scalar of a vote: r = a + b * LAMBDA (mod r) with a = bits 0..31, b = bits 32..63 of its
+# 64-bit SplitMix64 value. LAMBDA = -x^2 is the eigenvalue of phi on G1 (phi(P) = [-x^2] P)
+# and of -psi^2 on G2 (psi(Q) = [x] Q), so [r] P = [a] P + [b] phi(P) and
+# [r] Q = [a] Q + [b] (-psi^2(Q)): one 32-step chain instead of 64. The 2^64 (a, b) pairs give
+# distinct r (no (da, db) with |da|, |db| < 2^32 has da = LAMBDA db mod r), so the batch check's
+# soundness stays 2^-64.
+LAMBDA = (-X_ABS * X_ABS) % R_ORDER
+
+
+def rlc_scalar(z: int) -> int:
+    """The effective RLC scalar of a vote from its 64-bit value z."""
+    return ((z & 0xFFFFFFFF) + (z >> 32) * LAMBDA) % R_ORDER
 
 
 def _f2pow(a, e):
@@ -140,8 +153,9 @@ BETA = _beta()
 
 
 class Alg:
-    def __init__(self, prog: Prog, inv_op: bool = False):
+    def __init__(self, prog: Prog, inv_op: bool = False, use_sop: bool = False):
         self.p = prog
+        self.use_sop = use_sop   # Fp2 products as two sum-of-products ops (ir.Prog.sop)
         self.inv_op = inv_op   # Fp inversion by the interpreter's one-lane binary Euclid
 
     # ---------------------------------------------------------------- Fp
@@ -206,6 +220,8 @@ class Alg:
             return self.f2_mul_c(a, (p.cval(b[0]), p.cval(b[1])))
         if p.is_const(a[0]) and p.is_const(a[1]):
             return self.f2_mul_c(b, (p.cval(a[0]), p.cval(a[1])))
+        if self.use_sop:   # schoolbook on two lanes: a0 b0 - a1 b1, a0 b1 + a1 b0 (no post-adds)
+            return (p.sop(a[0], b[0], -1, a[1], b[1]), p.sop(a[0], b[1], 1, a[1], b[0]))
         t0 = a[0] * b[0]
         t1 = a[1] * b[1]
         t2 = p.muls(a[0], 1, a[1], b[0], 1, b[1])
@@ -587,6 +603,37 @@ class Alg:
                 acc = tuple((p.selb(k, a_[0], t_[0]), p.selb(k, a_[1], t_[1])) for a_, t_ in zip(acc, t))
         return acc
 
+    def pt_selb(self, F, k, A, B, after=None):
+        """bit k of the vote's 64-bit RLC value ? B : A (not scheduled before `after`)"""
+        p = self.p
+        if F == "fp":
+            return tuple(p.selb(k, a, b, after) for a, b in zip(A, B))
+        return tuple((p.selb(k, a[0], b[0], after), p.selb(k, a[1], b[1], after)) for a, b in zip(A, B))
+
+    def pt_mul_glv(self, F, A, B, nbits: int = 32):
+        """[a] A + [b] B for the vote's RLC value (a = bits 0..31, b = bits 32..63), B = [LAMBDA] A
+        by an endomorphism (see LAMBDA): one double-and-add-always chain over 32 bits whose
+        addend (O, A, B or A + B) is picked by two selb levels; complete formulas."""
+        AB = self.pt_add(F, A, B)
+        O = self.pt_inf(F)
+        acc = None
+        for k in range(nbits - 1, -1, -1):
+            # the step's addend is selected once the previous step's sum exists
+            dep = None if acc is None else (acc[2] if F == "fp" else acc[2][0])
+            lo = self.pt_selb(F, k, O, A, dep)
+            hi = self.pt_selb(F, k, B, AB, dep)
+            ad = self.pt_selb(F, k + nbits, lo, hi, dep)
+            acc = ad if acc is None else self.pt_add(F, self.pt_dbl(F, acc), ad)
+        return acc
+
+    def g1_phi(self, A):
+        """phi(P) = (beta X : Y : Z) = [-x^2] P on G1."""
+        return (A[0] * self.p.const(BETA), A[1], A[2])
+
+    def g2_neg_psi2(self, A):
+        """-psi^2(Q) = [-x^2] Q on G2."""
+        return self.pt_neg("f2", self.g2_psi(self.g2_psi(A)))
+
     def pt_sel(self, F, f, A, B):
         p = self.p
         if F == "fp":
@@ -614,8 +661,7 @@ class Alg:
         """phi(P) == [-x^2] P  (P not infinity)."""
         t1 = self.pt_mul_fixed("fp", A, X_ABS)
         t2 = self.pt_mul_fixed("fp", t1, X_ABS)
-        phi = (A[0] * self.p.const(BETA), A[1], A[2])
-        return self.pt_eq("fp", phi, self.pt_neg("fp", t2)), t1
+        return self.pt_eq("fp", self.g1_phi(A), self.pt_neg("fp", t2)), t1
 
     def g2_in_group(self, A):
         """psi(Q) == [x] Q = -[|x|] Q  (Q not infinity)."""
@@ -755,14 +801,17 @@ class Alg:
 
     # ---------------------------------------------------------------- pairing
     def miller_loop(self, Pa, Q):
-        """f_{|x|,Q}(P) conjugated. Pa affine (xP, yP) in Fp; Q = (X, Y, Z) projective in E2."""
+        """f_{|x|,Q}(P) conjugated. Pa = (xP, yP) affine or (XP, YP, ZP) homogeneous projective
+        in Fp (every line then carries the factor ZP in Fp, which the final exponentiation
+        removes: no inversion); Q = (X, Y, Z) projective in E2."""
         p = self.p
-        xP, yP = Pa
+        xP, yP = Pa[0], Pa[1]
+        ZP = Pa[2] if len(Pa) == 3 else None
         XQ, YQ, ZQ = Q
         m3x = -(xP + xP + xP)
         y2 = yP + yP
-        xPZ = self.f2_mul_fp(ZQ, xP)   # xP ZQ
-        yPZ = self.f2_mul_fp(ZQ, yP)   # yP ZQ
+        xPZ = self.f2_mul_fp(ZQ, xP)   # xP ZQ (times ZP when projective)
+        yPZ = self.f2_mul_fp(ZQ, yP)   # yP ZQ (times ZP when projective)
         T = Q
         f = None
         for b in range(62, -1, -1):
@@ -772,6 +821,8 @@ class Alg:
             ZZ = self.f2_sqr(Z)
             E = self.f2_mul_c(ZZ, (12, 12))          # 3 b' Z^2
             l0 = self.f2_sub(YY, E)
+            if ZP is not None:
+                l0 = self.f2_mul_fp(l0, ZP)
             l1 = self.f2_mul_fp(XX, m3x)
             YZ = self.f2_mul(Y, Z)
             l4 = self.f2_mul_fp(YZ, y2)
@@ -791,6 +842,8 @@ class Alg:
                 th = self.f2_sub(self.f2_mul(Y, ZQ), self.f2_mul(YQ, Z))
                 lm = self.f2_sub(self.f2_mul(X, ZQ), self.f2_mul(XQ, Z))
                 l0 = self.f2_sub(self.f2_mul(th, XQ), self.f2_mul(lm, YQ))
+                if ZP is not None:
+                    l0 = self.f2_mul_fp(l0, ZP)
                 l1 = self.f2_neg(self.f2_mul(th, xPZ))
                 l4 = self.f2_mul(lm, yPZ)
                 T = self.pt_add("f2", T, Q)

@@ -28,7 +28,7 @@ P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB1
 HALF_P = (P - 1) // 2
 CMAX = 15
 
-HEAVY = {"muls", "sgn0", "lex", "inv"}
+HEAVY = {"muls", "sgn0", "lex", "inv", "sop"}
 LIGHT = {"lin", "sel", "eq", "and", "or", "xor", "st", "selb"}
 
 
@@ -53,14 +53,15 @@ class Val:
 
 
 class Op:
-    __slots__ = ("kind", "srcs", "coefs", "imm", "name")
+    __slots__ = ("kind", "srcs", "coefs", "imm", "name", "deps")
 
-    def __init__(self, kind, srcs=(), coefs=(), imm=0, name=None):
+    def __init__(self, kind, srcs=(), coefs=(), imm=0, name=None, deps=()):
         self.kind = kind
         self.srcs = tuple(srcs)    # value ids or None; (a, b, c, d) for muls/lin/eq
         self.coefs = tuple(coefs)  # (ca, cb, cc, cd) for muls/lin/eq
         self.imm = imm
         self.name = name
+        self.deps = tuple(deps)    # ordering-only predecessors (no data, no slot lifetime)
 
 
 def _norm_terms(terms):
@@ -158,11 +159,11 @@ class Prog:
     def output(self, name, v: Val):
         self.outputs[name] = v.id
 
-    def _op(self, kind, srcs, coefs=(), imm=0):
-        k = (kind, tuple(srcs), tuple(coefs), imm)
+    def _op(self, kind, srcs, coefs=(), imm=0, deps=()):
+        k = (kind, tuple(srcs), tuple(coefs), imm, tuple(deps))
         if k in self.cse:
             return Val(self, self.cse[k])
-        v = self._new(Op(kind, srcs, coefs, imm))
+        v = self._new(Op(kind, srcs, coefs, imm, deps=deps))
         self.cse[k] = v.id
         return v
 
@@ -243,6 +244,12 @@ class Prog:
         return self._op("muls", (a.id, b.id if b is not None else None, c.id, d.id if d is not None else None),
                         (1, sb if b is not None else 0, 1, sd if d is not None else 0))
 
+    def sop(self, a, c, s, b, d):
+        """a * c + s * b * d (s = +1 / -1): two products, one Montgomery reduction."""
+        if s > 0 and (b.id, d.id) < (a.id, c.id):
+            a, c, b, d = b, d, a, c
+        return self._op("sop", (a.id, b.id, c.id, d.id), (1, s, 1, 1))
+
     def sgn0(self, a):
         return self._op("sgn0", (a.id,))
 
@@ -264,11 +271,12 @@ class Prog:
             return x
         return self._op("sel", (f.id, x.id, y.id))
 
-    def selb(self, k, x, y):
-        """bit k of the unit's 64-bit scalar ? y : x"""
+    def selb(self, k, x, y, after=None):
+        """bit k of the unit's 64-bit scalar ? y : x. `after`: a value this select must not be
+        scheduled before (keeps selects of long-ready operands next to their use)."""
         if x.id == y.id:
             return x
-        return self._op("selb", (x.id, y.id), (), k)
+        return self._op("selb", (x.id, y.id), (), k, deps=(after.id,) if after is not None else ())
 
     def f_and(self, a, b):
         return self._op("and", (a.id, b.id))
@@ -292,9 +300,12 @@ class Prog:
     def _lin_terms(self, op):
         return [(c, v) for c, v in zip(op.coefs, op.srcs) if v is not None and c != 0]
 
-    def fuse(self):
-        """Merge single-use lin ops into their consumer: into a lin (<= 4 distinct terms, small
-        coefficients) or into the 2-term operand sums of muls / eq. Returns ops absorbed."""
+    def fuse(self, dup: bool = False):
+        """Merge lin ops into their consumers: into a lin (<= 4 distinct terms, small
+        coefficients) or into the 2-term operand sums of muls / eq. A single-use producer is
+        absorbed when the consumer's coefficient form costs no more than the two did; with
+        `dup`, a shared producer is also copied into consumers whose form stays as cheap, which
+        takes it off their dependency chains. Returns ops absorbed."""
         live = set(self.live_ops())
         outs = set(self.outputs.values())
         uses = [0] * len(self.ops)
@@ -309,7 +320,7 @@ class Prog:
             return FORM_COST[f] if limit == 4 else (0 if f == "unit" else 1000)  # muls operands: unit only
 
         def fusable(j):
-            return j is not None and self.ops[j].kind == "lin" and uses[j] == 1 and j not in outs
+            return j is not None and self.ops[j].kind == "lin" and j not in outs and (uses[j] == 1 or dup)
 
         def try_merge(terms, limit):
             nonlocal absorbed
@@ -320,8 +331,11 @@ class Prog:
                     if fusable(v):
                         sub = [(c * c2, v2) for c2, v2 in self._lin_terms(self.ops[v])]
                         cand = _norm_terms(terms[:k] + terms[k + 1:] + sub)
+                        # a single-use producer disappears (its cost is credited); a shared one
+                        # is duplicated into this consumer only if the consumer gets no dearer
+                        credit = cost(self._lin_terms(self.ops[v]), 4) if uses[v] == 1 else 0
                         if len(cand) <= limit and all(abs(c3) <= CMAX for c3, _ in cand) and \
-                                cost(cand, limit) <= cost(terms, limit) + cost(self._lin_terms(self.ops[v]), 4):
+                                cost(cand, limit) <= cost(terms, limit) + credit:
                             uses[v] -= 1
                             for _, v2 in sub:
                                 uses[v2] += 1
@@ -395,6 +409,8 @@ def eval_op(op, vals, inputs, scalar):
         if k == "muls":
             return x * y % P
         return 1 if x == y else 0
+    if k == "sop":
+        return (g(0) * g(2) + op.coefs[1] * g(1) * g(3)) % P
     if k == "sgn0":
         return vals[s[0]] & 1
     if k == "lex":

@@ -10,8 +10,11 @@ layouts. Input and output names are listed in the order the HIP side addresses t
 """
 from __future__ import annotations
 
+
 from alg import G1X, G1Y, Alg
 from ir import P, Prog
+
+USE_SOP = False   # Fp2 products as sum-of-products ops (two lanes, no post-adds)
 
 R_MONT = pow(2, 384, P)
 
@@ -53,7 +56,7 @@ VOTE_ST = [(n, S_F + k) for k, n in enumerate(f12_names("f"))] + \
 
 def build_vote():
     p = Prog("vote")
-    a = Alg(p)
+    a = Alg(p, use_sop=USE_SOP)
     R = p.const(R_MONT)
     pkx = p.input("pk_x") * R
     sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
@@ -67,8 +70,8 @@ def build_vote():
     sig_grp = a.g2_in_group(Qs)
     H = a.hash_to_g2(u0, u1)
     h_inf = a.f2_is_zero(H[2])
-    rP = a.to_affine("fp", a.pt_mul_rbits("fp", Pp, 64))
-    rS = a.pt_mul_rbits("f2", Qs, 64)
+    rP = a.pt_mul_glv("fp", Pp, a.g1_phi(Pp))          # projective: no inversion
+    rS = a.pt_mul_glv("f2", Qs, a.g2_neg_psi2(Qs))
     f = a.miller_loop(rP, H)
     for name, v in zip(VOTE_OUT, [pk_ok, pk_grp, sig_ok, sig_grp, h_inf]):
         p.output(name, v)
@@ -85,7 +88,7 @@ FOLD_OUT = f12_names("F") + g2p_names("S")
 
 def build_fold():
     p = Prog("fold")
-    a = Alg(p)
+    a = Alg(p, use_sop=USE_SOP)
     Fs, Ss = [], []
     for k in range(FOLD_K):
         Fs.append(unflat12([p.input(n) for n in f12_names("F%d_" % k)]))
@@ -107,7 +110,7 @@ FINAL_OUT = ["ok"]
 
 def build_final():
     p = Prog("final")
-    a = Alg(p, inv_op=True)
+    a = Alg(p, inv_op=True, use_sop=USE_SOP)
     Fs, Ss = [], []
     for k in range(FOLD_K):
         Fs.append(unflat12([p.input(n) for n in f12_names("F%d_" % k)]))
@@ -130,7 +133,7 @@ PAIRCHK_OUT = ["ok"]
 
 def build_pairchk():
     p = Prog("pairchk")
-    a = Alg(p)
+    a = Alg(p, use_sop=USE_SOP)
     pk = (p.input("pkx"), p.input("pky"))
     sig = ((p.input("sx0"), p.input("sx1")), (p.input("sy0"), p.input("sy1")), (p.one, p.zero))
     H = unflat_g2p([p.input(n) for n in g2p_names("h")])

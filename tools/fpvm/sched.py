@@ -11,6 +11,7 @@ Instruction (4 x uint32 per lane per phase):
   w0 = opcode | dst << 5 (11 bits) | imm << 16 (6 bits)
   w1 = A | B << 16,  w2 = C | D << 16
   w3 = ca | cb << 5 | cc << 10 | cd << 15   (5-bit two's-complement coefficients)
+       (sop: z = A C + cb B D)
        | k << 20 (lin: k * (unit sum) when 2 <= k <= 15, ir.lin_form "scaled")
   operand: slot index (< CONST_BASE) or CONST_BASE + k (constant table entry k); a missing
   operand is the zero constant with coefficient 0, so every lane loads four operands.
@@ -23,7 +24,7 @@ from collections import defaultdict
 from ir import CMAX, HALF_P, HEAVY, P, lin_form
 
 OPC = {"nop": 0, "muls": 1, "sgn0": 2, "lex": 3, "inv": 4, "lin": 5, "sel": 6, "eq": 7, "and": 8, "or": 9,
-       "xor": 10, "st": 11, "selb": 12}
+       "xor": 10, "st": 11, "selb": 12, "sop": 13}
 CONST_BASE = 0x800
 ABSENT = 0xFFFF
 R_MONT = pow(2, 384, P)
@@ -75,7 +76,8 @@ class Scheduled:
                 "cost_est": heavy_rounds * 900 + (self.nrounds - heavy_rounds) * 150}
 
 
-def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1, mixed=True, slot_target=None):
+def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1, mixed=True, slot_target=None,
+             hoist=None, stretch=1.3):
     ops = prog.ops
     live = prog.live_ops()
     liveset = set(live)
@@ -85,6 +87,7 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
     succs = defaultdict(list)
     for i in work:
         ps = {s for s in ops[i].srcs if s is not None and s not in pre}
+        ps |= {s for s in ops[i].deps if s in liveset and s not in pre}   # ordering-only edges
         preds[i] = ps
         for s in ps:
             succs[s].append(i)
@@ -94,6 +97,17 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
         prio[i] = c + max((prio[s] for s in succs[i]), default=0)
         if ops[i].kind == "st":
             prio[i] = 10 ** 6   # stores free their slot: run them as soon as they are ready
+    # release phase: an op may not run more than `hoist` phases before the earliest phase its
+    # first consumer could run (ASAP depth x the schedule's expected stretch), so values that
+    # are ready early but needed late (the per-step addends of a scalar-multiplication chain)
+    # do not hold slots for hundreds of phases
+    asap = {}
+    for i in work:
+        asap[i] = 1 + max((asap[p_] for p_ in preds[i]), default=0)
+    release = {}
+    for i in work:
+        use = min((asap[c] for c in succs[i]), default=asap[i])
+        release[i] = max(0, int(stretch * use) - hoist) if hoist is not None else 0
     indeg = {i: len(preds[i]) for i in work}
     # remaining consumers of each slot value (inputs included), for register-pressure control
     remaining = defaultdict(int)
@@ -119,8 +133,10 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
             return []
         if pressure:
             cands.sort(key=lambda i: (delta(i), -prio[i]))
-        else:
-            cands.sort(key=lambda i: -prio[i])
+            take = cands[:n]
+            del cands[:n]
+            return take
+        cands.sort(key=lambda i: -prio[i])
         take = cands[:n]
         del cands[:n]
         return take
@@ -128,17 +144,27 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
     kinds = []
     done = 0
     while done < len(work):
+        t = len(rounds)
         pressure = slot_target is not None and live_now >= slot_target
-        top_h = max((prio[i] for i in ready_h), default=-1)
-        top_l = max((prio[i] for i in ready_l), default=-1)
-        if top_l > top_h or not ready_h:
+        # ops past their release phase are eligible; the rest wait (unless nothing is eligible)
+        eh = [i for i in ready_h if release[i] <= t]
+        el = [i for i in ready_l if release[i] <= t]
+        if not eh and not el:
+            eh, el = list(ready_h), list(ready_l)
+        wait_h = [i for i in ready_h if i not in set(eh)]
+        wait_l = [i for i in ready_l if i not in set(el)]
+        top_h = max((prio[i] for i in eh), default=-1)
+        top_l = max((prio[i] for i in el), default=-1)
+        if top_l > top_h or not eh:
             kind = "L"
-            cur = pick(ready_l, W, pressure)
+            cur = pick(el, W, pressure)
         else:
             kind = "H"
-            cur = pick(ready_h, W, pressure)
+            cur = pick(eh, W, pressure)
             if mixed:
-                cur += pick(ready_l, W - len(cur), pressure)
+                cur += pick(el, W - len(cur), pressure)
+        ready_h[:] = eh + wait_h
+        ready_l[:] = el + wait_l
         if not cur:
             raise RuntimeError("deadlock in scheduler")
         rounds.append(cur)
@@ -258,6 +284,9 @@ def encode(sc):
                         else:
                             C, D = u[0][1], u[1][1]
                         coefs[h], coefs[h + 1] = u[0][0], u[1][0]
+            elif k == "sop":           # A C + cb B D
+                A, B, C, D = s
+                coefs = op.coefs
             elif k in ("sgn0", "lex"):
                 A, B, C, D = s[0], None, None, None
                 coefs = (1, 0, 1, 0)
@@ -325,6 +354,8 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
                 continue
             elif opc == OPC["inv"]:
                 z = pow(A, P - 2, P)
+            elif opc == OPC["sop"]:
+                z = (A * C + cb * B * D) % P
             elif opc == OPC["lin"]:
                 z = (ca * A + cb * B + cc * C + cd * D) % P
                 if (w3 >> 20) & 15 > 1:
