@@ -183,11 +183,44 @@ __device__ __forceinline__ void slot_put(uint32_t* slots, uint32_t s, const uint
 
 __device__ __forceinline__ uint32_t slot_flag_get(const uint32_t* slots, uint32_t s) { return slots[s * 12]; }
 
+// One fold unit on a 16-lane slice: out[t] = (prod F, sum S) over in[4t .. 4t+3] (missing ->
+// identity); with codes (level 0) every vote whose code is not 0 contributes the identity.
+// All 64 threads of the workgroup call it (the phase barrier); `active` marks the working slice.
+__device__ __forceinline__ void fold_unit(uint32_t t, uint32_t m, const VmDev& prog, const uint32_t* cst,
+                                          uint32_t* slots, uint32_t lane, bool active, Slab inF, Slab inS,
+                                          Slab out, const int32_t* __restrict__ codes) {
+  if (active) {
+    for (uint32_t k = lane; k < 4 * PART_PLANES; k += VM_FOLD_W) {
+      const uint32_t q = k / PART_PLANES, j = k % PART_PLANES, e = 4 * t + q;
+      Fp v;
+      if (e < m && (!codes || codes[e] == 0)) {
+        if (j < 12) inF.ld(v, j, e);
+        else inS.ld(v, j - 12, e);
+      } else if (j == 0 || j == 12 + 2) {
+        fp_one(v);
+      } else {
+        fp_zero(v);
+      }
+      slot_put(slots, VM_FOLD_IN[k], v.v);
+    }
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  if (active) {
+    for (uint32_t k = lane; k < PART_PLANES; k += VM_FOLD_W) {
+      Fp v;
+      const uint32_t src = VM_FOLD_OUT[k];
+      for (int q = 0; q < 12; ++q) v.v[q] = slots[src * 12 + q];
+      out.st(v, k, t);
+    }
+  }
+}
+
 // Per vote: VM "vote" program + reference-precedence code + the vote's (f, r sigma)
 // contribution. LDS: constants, then VM_SLICES x (VM_VOTE_NSLOTS slots).
-__global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
+__global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
                                                 const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
-                                                Slab s, uint64_t seed, int32_t* __restrict__ codes) {
+                                                Slab s, uint64_t seed, int32_t* __restrict__ codes, Slab part0) {
   __builtin_amdgcn_s_setprio(2);  // per-vote stages outrank a co-resident final-stream wave
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
@@ -248,47 +281,32 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, const ui
     else c = 0;
     codes[i] = c;
   }
+  // fold level 0, fused: this workgroup's 4 votes -> partial blockIdx.x of part0 (F planes
+  // 0..11, S planes 12..17), the identity for failed votes. The slices' `st` outputs (HBM)
+  // and codes are made visible to the workgroup first; the fold reuses the vote slots' LDS.
+  __threadfence();
+  __syncthreads();
+  fold_unit(blockIdx.x, n, fold, cst, lds + VM_NCONST * 12, threadIdx.x % VM_FOLD_W,
+            threadIdx.x < VM_FOLD_W && 4 * blockIdx.x < n,
+            Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{s.p + (size_t)S_RS * 12 * s.cap, s.cap}, part0,
+            codes);
 }
 
-// Fold: out[t] = (prod F, sum S) over in[4t .. 4t+3] (missing -> identity).
-// Level 0 (codes != nullptr) takes the identity for every vote whose code is not 0.
+// Fold level: SLICES units per 64-thread workgroup (4 on the main stream; 1 on the final
+// stream, whose 10.8 KB of LDS fits beside a CU's four vote workgroups).
+template <int SLICES>
 __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
                                                 Slab inS, Slab out, const int32_t* __restrict__ codes) {
-  __builtin_amdgcn_s_setprio(2);  // per-vote stages outrank a co-resident final-stream wave
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
   const uint32_t slice = threadIdx.x / VM_FOLD_W, lane = threadIdx.x % VM_FOLD_W;
-  uint32_t* slots = lds + VM_NCONST * 12 + slice * VM_FOLD_NSLOTS * 12;
-  const uint32_t t = blockIdx.x * VM_SLICES + slice;
-  const bool active = 4 * t < m;
+  const uint32_t sl = slice < SLICES ? slice : 0;  // idle slices address slice 0 (never write)
+  uint32_t* slots = lds + VM_NCONST * 12 + sl * VM_FOLD_NSLOTS * 12;
+  const uint32_t t = blockIdx.x * SLICES + slice;
+  const bool active = slice < SLICES && 4 * t < m;
   load_consts(cst, cst_g, VM_NCONST);
-  if (active) {
-    for (uint32_t k = lane; k < 4 * PART_PLANES; k += VM_FOLD_W) {
-      const uint32_t q = k / PART_PLANES, j = k % PART_PLANES, e = 4 * t + q;
-      Fp v;
-      if (e < m && (!codes || codes[e] == 0)) {
-        if (j < 12) inF.ld(v, j, e);
-        else inS.ld(v, j - 12, e);
-      } else if (j == 0 || j == 12 + 2) {
-        fp_one(v);
-      } else {
-        fp_zero(v);
-      }
-      slot_put(slots, VM_FOLD_IN[k], v.v);
-    }
-  }
-  __syncthreads();
-  vm::run(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0},
-          blockIdx.x == 0 ? prog.trace : nullptr);
-  if (active) {
-    for (uint32_t k = lane; k < PART_PLANES; k += VM_FOLD_W) {
-      Fp v;
-      const uint32_t src = VM_FOLD_OUT[k];
-      for (int q = 0; q < 12; ++q) v.v[q] = slots[src * 12 + q];
-      out.st(v, k, t);
-    }
-  }
+  fold_unit(t, m, prog, cst, slots, lane, active, inF, inS, out, codes);
 }
 
 // Final: prod F * Miller(-G1, sum S) over in[0..m-1] (m <= 4) -> FE == 1 -> *result.
@@ -341,22 +359,6 @@ __global__ __launch_bounds__(64) void k_vm_pairchk(uint32_t n, VmDev prog, const
   vm::run(prog.code, VM_PAIRCHK_NPHASES, VM_PAIRCHK_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0},
           blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) codes[i] = slot_flag_get(slots, VM_PAIRCHK_OUT[0]) ? 0 : BLST_VERIFY_FAIL;
-}
-
-// the <= 4 fold outputs (F planes 0..11, S planes 0..5) -> a private plane set (cap 4) that the
-// final stream reads while the next batch reuses the fold scratch
-__global__ __launch_bounds__(64) void k_copy_parts(uint32_t m, Slab F, Slab S, Slab oF, Slab oS) {
-  for (uint32_t t = threadIdx.x; t < m * PART_PLANES; t += 64) {
-    const uint32_t q = t / PART_PLANES, j = t % PART_PLANES;
-    Fp v;
-    if (j < 12) {
-      F.ld(v, j, q);
-      oF.st(v, j, q);
-    } else {
-      S.ld(v, j - 12, q);
-      oS.st(v, j - 12, q);
-    }
-  }
 }
 
 // AoS partials (216 words: F 144, S 72) -> planes
@@ -577,7 +579,10 @@ static constexpr size_t LDS_FINAL = (size_t)VM_NCONST * 48 + (size_t)VM_FINAL_NS
 static constexpr size_t LDS_PAIRCHK = (size_t)VM_NCONST * 48 + VM_SLICES * (size_t)VM_PAIRCHK_NSLOTS * 48;
 static_assert(VM_VOTE_W * VM_SLICES == 64 && VM_FOLD_W * VM_SLICES == 64 && VM_PAIRCHK_W * VM_SLICES == 64 &&
                   VM_FINAL_W == 64, "VM slice widths");
+static constexpr size_t LDS_FOLD1 = (size_t)VM_NCONST * 48 + (size_t)VM_FOLD_NSLOTS * 48;
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
+static_assert(VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_NSLOTS * 12 + 4), "fused fold reuses the vote slots");
+static_assert(VM_FOLD_W == VM_VOTE_W, "fused fold slice width");
 
 static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphases, uint32_t W, const uint16_t* in,
                      uint32_t nin, const uint16_t* out, uint32_t nout) {
@@ -621,7 +626,9 @@ static int vm_init(ovh_ctx* c) {
                 VM_PAIRCHK_NIN, VM_PAIRCHK_OUT, VM_PAIRCHK_NOUT))
     return OVH_ERR_DEVICE;
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE));
-  HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FOLD));
+  HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold<VM_SLICES>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)LDS_FOLD));
+  HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FOLD1));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FINAL));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_pairchk, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)LDS_PAIRCHK));
@@ -1027,45 +1034,51 @@ int ovh_verify_aggregated(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, co
 }
 
 // ---- batch ----
-// Per-vote stages + fold tree down to <= 4 partials (*outF / *outS planes, *out_m elements).
+// Per-vote stages of a batch on the main stream: hash_to_field, then the vote kernel with fold
+// level 0 fused in: *outF / *outS = ceil(n / 4) partials as planes in the slot's fold scratch
+// (half 0), *out_m their count.
 static int batch_front(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
                        uint64_t seed, int32_t* d_codes, Slab* outF, Slab* outS, uint32_t* out_m) {
   Slab s{c->state, c->cap};
   hipStream_t st = c->stream;
   c->ev_mask = 0;
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
+  Slab p0{c->red, c->red_cap};
   { StageScope p(c, ST_H2F); k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s); }
   {
     StageScope p(c, ST_VOTE);
-    k_vm_vote<<<nwg, 64, LDS_VOTE, st>>>(n, c->vm_vote, c->vm_consts, d_pks, d_sigs, s, seed, d_codes);
-  }
-  HIPCHK(hipGetLastError());
-  // fold tree: level 0 reads the state planes (F at S_F, S at S_RS), later levels the
-  // ping-pong scratch (F planes 0..11, S planes 12..17)
-  Slab inF{c->state + (size_t)S_F * 12 * c->cap, c->cap}, inS{c->state + (size_t)S_RS * 12 * c->cap, c->cap};
-  uint32_t m = n;
-  int flip = 0;
-  {
-    StageScope p(c, ST_FOLD);
-    // at least one level: level 0 substitutes the identity for failed votes
-    do {
-      const uint32_t mo = (m + 3) / 4;
-      uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
-      Slab o{base, c->red_cap};
-      k_vm_fold<<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, st>>>(m, c->vm_fold, c->vm_consts, inF, inS, o,
-                                                                       m == n ? d_codes : nullptr);
-      inF = o;
-      inS = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
-      m = mo;
-      flip ^= 1;
-    } while (m > 4);
+    k_vm_vote<<<nwg, 64, LDS_VOTE, st>>>(n, c->vm_vote, c->vm_fold, c->vm_consts, d_pks, d_sigs, s, seed, d_codes,
+                                         p0);
   }
   HIPCHK(hipGetLastError());
   c->last_n = n;
-  *outF = inF;
-  *outS = inS;
-  *out_m = m;
+  *outF = p0;
+  *outS = Slab{c->red + (size_t)12 * 12 * c->red_cap, c->red_cap};
+  *out_m = nwg;
   return 0;
+}
+
+// Remaining fold levels down to <= 4 partials, on stream st, ping-ponging through the slot's
+// fold scratch (the level-0 partials are in half 0). slices = 4 (main stream) or 1 (the final
+// stream, beside the next batch's vote workgroups).
+static int fold_levels(ovh_ctx* c, hipStream_t st, int slices, Slab* F, Slab* S, uint32_t* m) {
+  StageScope p(c, ST_FOLD, st);
+  int flip = 1;
+  while (*m > 4) {
+    const uint32_t mo = (*m + 3) / 4;
+    uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
+    Slab o{base, c->red_cap};
+    if (slices == 1)
+      k_vm_fold<1><<<mo, 64, LDS_FOLD1, st>>>(*m, c->vm_fold, c->vm_consts, *F, *S, o, nullptr);
+    else
+      k_vm_fold<VM_SLICES><<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, st>>>(*m, c->vm_fold, c->vm_consts, *F,
+                                                                                 *S, o, nullptr);
+    *F = o;
+    *S = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
+    *m = mo;
+    flip ^= 1;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
 }
 
 // Verdict words in c->result: [0] single-call APIs, [8 + slot] pipelined batches,
@@ -1092,11 +1105,11 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   Slab F, S;
   uint32_t m;
   int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m);
-  if (e) return e;
+  if (e || (e = fold_levels(c, c->stream, VM_SLICES, &F, &S, &m))) return e;
   if (m > 1) {  // fold the last <= 4 into one partial
     uint32_t* base = c->red + (size_t)(F.p == c->red ? 1 : 0) * PART_PLANES * 12 * c->red_cap;
     Slab o{base, c->red_cap};
-    k_vm_fold<<<1, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o, nullptr);
+    k_vm_fold<VM_SLICES><<<1, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o, nullptr);
     F = o;
   }
   // pack element 0 (F planes, S planes) into the AoS partial
@@ -1136,7 +1149,7 @@ static int stage_partials(ovh_ctx* c, hipStream_t st, size_t k, const uint8_t* d
   } else {
     uint32_t* o = scratch + (size_t)PART_PLANES * 12 * 16;
     Slab oF{o, 4};
-    k_vm_fold<<<1, 64, LDS_FOLD, st>>>((uint32_t)k, c->vm_fold, c->vm_consts, uF, uS, oF, nullptr);
+    k_vm_fold<VM_SLICES><<<1, 64, LDS_FOLD, st>>>((uint32_t)k, c->vm_fold, c->vm_consts, uF, uS, oF, nullptr);
     *F = oF;
     *S = Slab{o + (size_t)12 * 12 * 4, 4};
     *m = (uint32_t)((k + 3) / 4);
@@ -1160,8 +1173,8 @@ int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials)
     const uint32_t mo = (m + 3) / 4;
     uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
     Slab o{base, c->red_cap};
-    k_vm_fold<<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o,
-                                                                            nullptr);
+    k_vm_fold<VM_SLICES><<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts,
+                                                                                       F, S, o, nullptr);
     F = o;
     S = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
     m = mo;
@@ -1220,15 +1233,12 @@ int ovh_verify_batch_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, c
   uint32_t m;
   int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m);
   if (e) return e;
-  // hand the <= 4 fold outputs to the final stream through the slot's private copy
-  uint32_t* fb = c->fin + (size_t)slot * FIN_STRIDE;
-  Slab oF{fb, 4}, oS{fb + (size_t)12 * 12 * 4, 4};
-  k_copy_parts<<<1, 64, 0, c->stream>>>(m, F, S, oF, oS);
-  HIPCHK(hipGetLastError());
+  // the final stream takes over the slot: remaining fold levels, combined check, fallback
   HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
   HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_front[slot], 0));
+  if ((e = fold_levels(c, c->fstream, 1, &F, &S, &m))) return e;
   int32_t* verdict = c->result + RES_BATCH + slot;
-  enqueue_final(c, c->fstream, oF, oS, m, verdict);
+  enqueue_final(c, c->fstream, F, S, m, verdict);
   enqueue_fallback(c, c->fstream, slot, (uint32_t)n, d_codes, verdict);
   HIPCHK(hipEventRecord(c->ev_back[slot], c->fstream));
   HIPCHK(hipGetLastError());
