@@ -298,11 +298,13 @@ __device__ __forceinline__ void run(const uint4* __restrict__ code, uint32_t nph
                                     uint64_t scalar, const Out& out, uint64_t* __restrict__ trace = nullptr) {
   // trace (diagnostics, OVH_FLAG_VM_TRACE): wall clock after every phase barrier
   if (trace && threadIdx.x == 0) trace[0] = wall_clock64();
-  uint4 nxt = code[lane];
+  // instructions are prefetched two phases ahead (an HBM/L2 round trip outlasts a light phase)
+  uint4 nxt = code[lane], nxt2 = code[(size_t)W + lane];
 #pragma unroll 1
   for (uint32_t ph = 0; ph < nphases; ++ph) {
     const uint4 cur = nxt;
-    nxt = code[(size_t)(ph + 1) * W + lane];  // code carries one trailing NOP phase
+    nxt = nxt2;
+    nxt2 = code[(size_t)(ph + 2) * W + lane];  // code carries two trailing NOP phases
     exec(cur, active, slots, cst, scalar, out);
     // The VM kernels are single-wave workgroups: the phase's slot writes are visible to the
     // next phase's reads once this wave's LDS operations completed (lgkmcnt(0)); the barrier

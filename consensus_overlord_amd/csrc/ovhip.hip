@@ -586,7 +586,7 @@ static_assert(VM_FOLD_W == VM_VOTE_W, "fused fold slice width");
 
 static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphases, uint32_t W, const uint16_t* in,
                      uint32_t nin, const uint16_t* out, uint32_t nout) {
-  const size_t words = (size_t)nphases * W * 4, pad = (size_t)W * 4;  // + one NOP phase
+  const size_t words = (size_t)nphases * W * 4, pad = (size_t)2 * W * 4;  // + two NOP phases (prefetch)
   void *dc = nullptr, *di = nullptr, *dout = nullptr;
   HIPCHK(hipMalloc(&dc, (words + pad) * 4));
   c->vm_bufs.push_back(dc);

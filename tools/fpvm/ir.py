@@ -53,7 +53,7 @@ class Val:
 
 
 class Op:
-    __slots__ = ("kind", "srcs", "coefs", "imm", "name", "deps")
+    __slots__ = ("kind", "srcs", "coefs", "imm", "name", "deps", "sec")
 
     def __init__(self, kind, srcs=(), coefs=(), imm=0, name=None, deps=()):
         self.kind = kind
@@ -62,6 +62,7 @@ class Op:
         self.imm = imm
         self.name = name
         self.deps = tuple(deps)    # ordering-only predecessors (no data, no slot lifetime)
+        self.sec = None            # program section that created it (diagnostics)
 
 
 def _norm_terms(terms):
@@ -131,6 +132,7 @@ class Prog:
 
     # ------------------------------------------------------------------ builders
     def _new(self, op):
+        op.sec = getattr(self, "section", None)
         self.ops.append(op)
         return Val(self, len(self.ops) - 1)
 

@@ -61,7 +61,7 @@ int main() {
   const char* names[] = {"nop", "lin", "muls", "muls_half_lanes", "lin_coef", "muls_preadd"};
   for (uint32_t W : {16u, 64u}) {
     for (int kind = 0; kind < 6; ++kind) {
-      std::vector<uint32_t> code((size_t)(NPH + 1) * W * 4, 0);
+      std::vector<uint32_t> code((size_t)(NPH + 2) * W * 4, 0);
       for (uint32_t ph = 0; ph < NPH; ++ph)
         for (uint32_t l = 0; l < W; ++l) {
           uint32_t* c = &code[((size_t)ph * W + l) * 4];
