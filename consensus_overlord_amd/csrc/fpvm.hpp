@@ -90,6 +90,16 @@ VM_FN void acc_bias(uint32_t* acc, int k) {
 // carries a relative error < 3 * 2^-24 and is shrunk by 2^-20, so f <= r and
 // floor(f) >= floor(r) - 1: q = floor(f) is at most floor(acc / p) and at most 2 short of it.
 // Subtract q p, then two conditional subtractions.
+// 2p as 12 limbs + a top limb
+constexpr uint32_t P2_LIMBS[12] = {
+    P_LIMBS[0] << 1, (P_LIMBS[1] << 1) | (P_LIMBS[0] >> 31), (P_LIMBS[2] << 1) | (P_LIMBS[1] >> 31),
+    (P_LIMBS[3] << 1) | (P_LIMBS[2] >> 31), (P_LIMBS[4] << 1) | (P_LIMBS[3] >> 31),
+    (P_LIMBS[5] << 1) | (P_LIMBS[4] >> 31), (P_LIMBS[6] << 1) | (P_LIMBS[5] >> 31),
+    (P_LIMBS[7] << 1) | (P_LIMBS[6] >> 31), (P_LIMBS[8] << 1) | (P_LIMBS[7] >> 31),
+    (P_LIMBS[9] << 1) | (P_LIMBS[8] >> 31), (P_LIMBS[10] << 1) | (P_LIMBS[9] >> 31),
+    (P_LIMBS[11] << 1) | (P_LIMBS[10] >> 31)};
+constexpr uint32_t P2_TOP = P_LIMBS[11] >> 31;
+
 VM_FN void acc_reduce(Fp& r, uint32_t* acc) {
   const uint64_t top = ((uint64_t)acc[12] << 32) | acc[11];  // acc >> 352
   constexpr float QS = (float)((1.0 - 0x1p-20) / ((double)P_LIMBS[11] + 1.0));
@@ -102,17 +112,18 @@ VM_FN void acc_reduce(Fp& r, uint32_t* acc) {
     acc[j] = subc32(acc[j], (uint32_t)pr, br, &br);
   }
   acc[12] = acc[12] - (uint32_t)(pr >> 32) - br;
+  // acc is now below 3p: acc - p and acc - 2p as two interleaved borrow chains, keep the
+  // smallest non-negative of acc, acc - p, acc - 2p
+  uint32_t d1[13], d2[13], b1 = 0, b2 = 0;
 #pragma unroll
-  for (int round = 0; round < 2; ++round) {
-    uint32_t d[13];
-    br = 0;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) d[j] = subc32(acc[j], P_LIMBS[j], br, &br);
-    d[12] = subc32(acc[12], 0u, br, &br);
-    const bool keep = br != 0;
-#pragma unroll
-    for (int j = 0; j < 13; ++j) acc[j] = keep ? acc[j] : d[j];
+  for (int j = 0; j < 12; ++j) {
+    d1[j] = subc32(acc[j], P_LIMBS[j], b1, &b1);
+    d2[j] = subc32(acc[j], P2_LIMBS[j], b2, &b2);
   }
+  d1[12] = subc32(acc[12], 0u, b1, &b1);
+  d2[12] = subc32(acc[12], P2_TOP, b2, &b2);
+#pragma unroll
+  for (int j = 0; j < 13; ++j) acc[j] = !b2 ? d2[j] : (!b1 ? d1[j] : acc[j]);
 #pragma unroll
   for (int j = 0; j < 12; ++j) r.v[j] = acc[j];
 }
@@ -178,17 +189,47 @@ VM_FN void fp_inv_binary(Fp& r, const Fp& a, const Fp& r3) {
 // constant when s = 0), branch-free: d = A + (s < 0 ? p - B : B) < 2p, then one conditional
 // subtraction of p.
 VM_FN void addsub(Fp& r, const Fp& A, const Fp& B, int s) {
-  uint32_t nb[12], d[12], t[12], br = 0, c = 0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) nb[j] = subc32(P_LIMBS[j], B.v[j], br, &br);
+  // the three carry chains (p - B, A + B', d - p) run skewed by one limb each and interleave, so
+  // no chain's carry read directly follows its own carry write (gfx950 wait states)
+  uint32_t nb[12], d[12], t[12], b0 = 0, c1 = 0, b2 = 0;
   const bool ng = s < 0;
 #pragma unroll
-  for (int j = 0; j < 12; ++j) d[j] = addc32(A.v[j], ng ? nb[j] : B.v[j], c, &c);
-  br = 0;
+  for (int j = 0; j < 14; ++j) {
+    if (j < 12) nb[j] = subc32(P_LIMBS[j], B.v[j], b0, &b0);
+    if (j >= 1 && j <= 12) d[j - 1] = addc32(A.v[j - 1], ng ? nb[j - 1] : B.v[j - 1], c1, &c1);
+    if (j >= 2) t[j - 2] = subc32(d[j - 2], P_LIMBS[j - 2], b2, &b2);
+  }
 #pragma unroll
-  for (int j = 0; j < 12; ++j) t[j] = subc32(d[j], P_LIMBS[j], br, &br);
+  for (int j = 0; j < 12; ++j) r.v[j] = b2 ? d[j] : t[j];
+}
+
+// Two independent addsubs with their carry chains interleaved limb by limb: on gfx950 a VALU
+// carry read right after the VALU carry write costs wait states (s_nop), which the other
+// chain's instruction fills.
+VM_FN void addsub2(Fp& r1, const Fp& A1, const Fp& B1, int s1, Fp& r2, const Fp& A2, const Fp& B2, int s2) {
+  uint32_t n1[12], n2[12], d1[12], d2[12], t1[12], t2[12], b1 = 0, b2 = 0, c1 = 0, c2 = 0;
 #pragma unroll
-  for (int j = 0; j < 12; ++j) r.v[j] = br ? d[j] : t[j];
+  for (int j = 0; j < 12; ++j) {
+    n1[j] = subc32(P_LIMBS[j], B1.v[j], b1, &b1);
+    n2[j] = subc32(P_LIMBS[j], B2.v[j], b2, &b2);
+  }
+  const bool g1 = s1 < 0, g2 = s2 < 0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    d1[j] = addc32(A1.v[j], g1 ? n1[j] : B1.v[j], c1, &c1);
+    d2[j] = addc32(A2.v[j], g2 ? n2[j] : B2.v[j], c2, &c2);
+  }
+  b1 = b2 = 0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    t1[j] = subc32(d1[j], P_LIMBS[j], b1, &b1);
+    t2[j] = subc32(d2[j], P_LIMBS[j], b2, &b2);
+  }
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    r1.v[j] = b1 ? d1[j] : t1[j];
+    r2.v[j] = b2 ? d2[j] : t2[j];
+  }
 }
 
 #if defined(__HIPCC__)
@@ -226,8 +267,7 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots,
   Fp z = A;
   if (wave_any(is_mul || is_lin)) {
     Fp x, y;
-    addsub(x, A, B, cb);
-    addsub(y, C, D, cc * cd);
+    addsub2(x, A, B, cb, y, C, D, cc * cd);
     if (wave_any(is_mul)) {
       Fp m;
       fp_mul(m, x, y);
