@@ -297,6 +297,7 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
 template <int SLICES>
 __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
                                                 Slab inS, Slab out, const int32_t* __restrict__ codes) {
+  __builtin_amdgcn_s_setprio(2);  // short: run ahead of a co-resident final wave
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -533,12 +534,13 @@ struct ovh_ctx {
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
   // pipelined batches (ovh_verify_batch_device_async): the final check + fallback of batch k run
-  // on fstream while batch k + 1's per-vote stages run on stream; two slots of batch state.
+  // on fstream while batch k + 1's per-vote stages run on stream; OVH_BATCH_SLOTS slots of batch
+  // state rotate (a slot is reused only after its final-stream work finished).
   hipStream_t fstream = nullptr;
-  hipEvent_t ev_front[2] = {}, ev_back[2] = {};
-  uint32_t* state_slot[2] = {};
-  uint32_t* red_slot[2] = {};
-  uint32_t* fin = nullptr;       // 4 x FIN_STRIDE words: per slot, the final's partials; combine scratch
+  hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
+  uint32_t* state_slot[OVH_BATCH_SLOTS] = {};
+  uint32_t* red_slot[OVH_BATCH_SLOTS] = {};
+  uint32_t* fin = nullptr;       // OVH_BATCH_SLOTS x FIN_STRIDE words: per-slot combine scratch
   uint32_t pipe_k = 0;
   int last_slot = 0;
   XmdTemplates xmd;
@@ -663,7 +665,7 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
   while (cap < n) cap <<= 1;
   HIPCHK(hipStreamSynchronize(c->stream));
   if (c->fstream) HIPCHK(hipStreamSynchronize(c->fstream));
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
     if (c->state_slot[k]) (void)hipFree(c->state_slot[k]);
     if (c->red_slot[k]) (void)hipFree(c->red_slot[k]);
     c->state_slot[k] = c->red_slot[k] = nullptr;
@@ -674,7 +676,7 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
   c->state = nullptr;
   c->red = nullptr;
   c->red_cap = cap / 4 > 64 ? cap / 4 : 64;
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
     HIPCHK(hipMalloc(&c->state_slot[k], (size_t)S_TOTAL * 12 * cap * 4));
     HIPCHK(hipMalloc(&c->red_slot[k], (size_t)2 * PART_PLANES * 12 * c->red_cap * 4));
   }
@@ -741,11 +743,11 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
     if (hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) != hipSuccess ||
-        hipMalloc(&c->fin, (size_t)4 * FIN_STRIDE * 4) != hipSuccess) {
+        hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) != hipSuccess) {
       ovh_destroy(c);
       return nullptr;
     }
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
       if (hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&c->ev_back[k], hipEventDisableTiming) != hipSuccess) {
         ovh_destroy(c);
@@ -766,12 +768,14 @@ void ovh_destroy(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->fstream) (void)hipStreamSynchronize(c->fstream);
-  for (void* p : {(void*)c->state_slot[0], (void*)c->state_slot[1], (void*)c->red_slot[0], (void*)c->red_slot[1],
-                  (void*)c->st_pk, (void*)c->st_sig, (void*)c->codes, (void*)c->in_buf, (void*)c->partial,
+  for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
+    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k]})
+      if (p) (void)hipFree(p);
+  for (void* p : {(void*)c->st_pk, (void*)c->st_sig, (void*)c->codes, (void*)c->in_buf, (void*)c->partial,
                   (void*)c->result, (void*)c->vm_consts, (void*)c->fin})
     if (p) (void)hipFree(p);
   if (c->fstream) (void)hipStreamDestroy(c->fstream);
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
     if (c->ev_front[k]) (void)hipEventDestroy(c->ev_front[k]);
     if (c->ev_back[k]) (void)hipEventDestroy(c->ev_back[k]);
   }
@@ -1058,13 +1062,15 @@ static int batch_front(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint
   return 0;
 }
 
-// Remaining fold levels down to <= 4 partials, on stream st, ping-ponging through the slot's
-// fold scratch (the level-0 partials are in half 0). slices = 4 (main stream) or 1 (the final
-// stream, beside the next batch's vote workgroups).
-static int fold_levels(ovh_ctx* c, hipStream_t st, int slices, Slab* F, Slab* S, uint32_t* m) {
+// Fold levels down to <= `until` partials, on stream st, ping-ponging through the slot's fold
+// scratch (the level-0 partials are in half 0; *flip_io carries the next output half across
+// calls). slices = 4 (main stream) or 1 (the final stream, beside the next batch's vote
+// workgroups).
+static int fold_levels(ovh_ctx* c, hipStream_t st, int slices, Slab* F, Slab* S, uint32_t* m, uint32_t until = 4,
+                       int* flip_io = nullptr) {
   StageScope p(c, ST_FOLD, st);
-  int flip = 1;
-  while (*m > 4) {
+  int flip = flip_io ? *flip_io : 1;
+  while (*m > until) {
     const uint32_t mo = (*m + 3) / 4;
     uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
     Slab o{base, c->red_cap};
@@ -1078,12 +1084,14 @@ static int fold_levels(ovh_ctx* c, hipStream_t st, int slices, Slab* F, Slab* S,
     *m = mo;
     flip ^= 1;
   }
+  if (flip_io) *flip_io = flip;
   return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
 }
 
-// Verdict words in c->result: [0] single-call APIs, [8 + slot] pipelined batches,
-// [10 + slot] pipelined combines, [12] synchronous combine.
-enum { RES_BATCH = 8, RES_COMBINE = 10, RES_SYNC = 12 };
+// Verdict words in c->result: [0] single-call APIs, then per batch slot the pipelined batch
+// and pipelined combine verdicts, then the synchronous combine's.
+enum { RES_BATCH = 4, RES_COMBINE = RES_BATCH + OVH_BATCH_SLOTS, RES_SYNC = RES_COMBINE + OVH_BATCH_SLOTS };
+static_assert(RES_SYNC < 16, "verdict words fit c->result");
 
 int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
                              uint64_t seed, int32_t* d_codes, uint8_t* d_partial) {
@@ -1101,7 +1109,7 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
     return 0;
   }
   if (ensure_cap(c, n)) return OVH_ERR_DEVICE;
-  if (take_slot(c, (int)(c->pipe_k++ & 1))) return OVH_ERR_DEVICE;
+  if (take_slot(c, (int)(c->pipe_k++ % OVH_BATCH_SLOTS))) return OVH_ERR_DEVICE;
   Slab F, S;
   uint32_t m;
   int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m);
@@ -1208,7 +1216,7 @@ int ovh_combine_partials_device_async(ovh_ctx* c, size_t k, const uint8_t* d_par
   if (n != c->last_n) return OVH_ERR_ARG;
   const int slot = c->last_slot;
   // the partials were produced (and gathered) before this call returned to the host
-  uint32_t* scratch = c->fin + (size_t)(2 + slot) * FIN_STRIDE;
+  uint32_t* scratch = c->fin + (size_t)slot * FIN_STRIDE;
   Slab F, S;
   uint32_t m;
   if (stage_partials(c, c->fstream, k, d_partials, scratch, &F, &S, &m)) return OVH_ERR_DEVICE;
@@ -1227,16 +1235,19 @@ int ovh_verify_batch_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, c
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   if (ensure_cap(c, n)) return OVH_ERR_DEVICE;
-  const int slot = (int)(c->pipe_k++ & 1);
+  const int slot = (int)(c->pipe_k++ % OVH_BATCH_SLOTS);
   if (take_slot(c, slot)) return OVH_ERR_DEVICE;
   Slab F, S;
   uint32_t m;
   int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m);
   if (e) return e;
-  // the final stream takes over the slot: remaining fold levels, combined check, fallback
+  // fold levels: the wide ones on the main stream (short, high priority), the narrow ones and
+  // the combined check + fallback on the final stream -- balancing the two streams' chains
+  int flip = 1;
+  if ((e = fold_levels(c, c->stream, VM_SLICES, &F, &S, &m, 64, &flip))) return e;
   HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
   HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_front[slot], 0));
-  if ((e = fold_levels(c, c->fstream, 1, &F, &S, &m))) return e;
+  if ((e = fold_levels(c, c->fstream, 1, &F, &S, &m, 4, &flip))) return e;
   int32_t* verdict = c->result + RES_BATCH + slot;
   enqueue_final(c, c->fstream, F, S, m, verdict);
   enqueue_fallback(c, c->fstream, slot, (uint32_t)n, d_codes, verdict);

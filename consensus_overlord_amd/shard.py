@@ -18,6 +18,7 @@ import torch
 import torch.distributed as dist
 
 PARTIAL_BYTES = 864
+BATCH_SLOTS = 2      # include/ovhip.h OVH_BATCH_SLOTS: batches in flight per context
 
 
 class DeviceBackend:
@@ -29,7 +30,7 @@ class DeviceBackend:
         self.dev = device
 
     def empty_partials(self, world: int) -> torch.Tensor:
-        return torch.empty((2, world, PARTIAL_BYTES), dtype=torch.uint8, device="cuda")
+        return torch.empty((BATCH_SLOTS, world, PARTIAL_BYTES), dtype=torch.uint8, device="cuda")
 
     def partial(self, sigs, hashes, pks, seed: int, codes, out_row) -> None:
         self.dev.batch_partial(self.ctx, sigs, hashes, pks, seed, codes, out_row)
@@ -50,7 +51,7 @@ class ShardVerifier:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.nccl = dist.get_backend(group) == "nccl"
-        self.partials = backend.empty_partials(self.world)   # two in flight (pipelining)
+        self.partials = backend.empty_partials(self.world)   # one per batch in flight (pipelining)
 
     def _all_gather(self, part: torch.Tensor) -> None:
         mine = part[self.rank].clone()
@@ -62,7 +63,7 @@ class ShardVerifier:
     def submit(self, s: int, sigs, hashes, pks, seed: int, codes) -> None:
         """Enqueue batch s: this rank's n votes -> partial -> all-gather -> combined check and
         (device-gated) fallback into `codes`, final after wait()."""
-        part = self.partials[s % 2]
+        part = self.partials[s % self.partials.shape[0]]
         seed = (seed ^ (self.rank * 0x9E3779B97F4A7C15)) & 0xFFFFFFFFFFFFFFFF   # rank-distinct RLC scalars
         self.backend.partial(sigs, hashes, pks, seed, codes, part[self.rank])
         self._all_gather(part)

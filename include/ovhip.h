@@ -109,9 +109,11 @@ int ovh_batch_fallback_device(ovh_ctx* ctx, size_t n, int32_t* d_codes);
 /* Pipelined batches. ovh_verify_batch_device_async enqueues one batch and returns without
  * waiting: the per-vote stages run on ovh_stream, the combined check and (device-gated) per-vote
  * fallback on a second, lower-priority stream, so batch k's final exponentiation overlaps batch
- * k + 1's per-vote work. Two batches may be in flight per context; d_codes of a batch must stay
- * untouched until ovh_batch_wait returns, after which they hold exactly the per-vote
- * ovh_verify results. ovh_verify_batch_device = the async call + ovh_batch_wait. */
+ * k + 1's per-vote work. Up to OVH_BATCH_SLOTS batches may be in flight per context; the
+ * d_codes of a batch must stay untouched until ovh_batch_wait returns, after which they hold
+ * exactly the per-vote ovh_verify results. ovh_verify_batch_device = the async call +
+ * ovh_batch_wait. */
+#define OVH_BATCH_SLOTS 2 /* batches in flight per context (state slots) */
 int ovh_verify_batch_device_async(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
                                   const uint8_t* d_pks, uint64_t seed, int32_t* d_codes);
 int ovh_batch_wait(ovh_ctx* ctx);
