@@ -256,3 +256,41 @@ def test_partials_interoperate_with_oracle(cc):
         parts[1] = torch.from_numpy(p1).cuda()
         assert dev.combine_partials(cc.ctx, parts) == want
         assert orc.combine_partials(parts.cpu().numpy()) == want
+
+
+def test_shard_verifier_rccl_single_rank(cc):
+    """The multi-GPU driver (consensus_overlord_amd/shard.py) on the GPU with libovhip as the
+    backend, over a one-rank RCCL group: pipelined shard batches (one with invalid votes) give
+    the per-vote codes."""
+    import os
+    import socket
+    import torch
+    import torch.distributed as dist
+    import bls12_381 as bls
+    from consensus_overlord_amd import device as dev
+    from consensus_overlord_amd.shard import DeviceBackend, ShardVerifier
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        n = 64
+        sks, hs = _synth(n, seed=55)
+        pks = dev.sk_to_pk_batch(cc.ctx, sks)
+        sigs = dev.sign_batch(cc.ctx, sks, hs)
+        s_host = sigs.cpu().numpy().copy()
+        pt = bls.g2_from_bytes(bytes(s_host[9]))
+        s_host[9] = np.frombuffer(bls.g2_compress(bls.pt_add(bls.Fp2Ops, pt, bls.G2_GEN)), dtype=np.uint8)
+        bad = torch.from_numpy(s_host).cuda()
+        sv = ShardVerifier(DeviceBackend(cc.ctx))
+        codes = torch.full((3, n), -1, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        for b, sg in enumerate((sigs, bad, sigs)):
+            sv.submit(b, sg, hs, pks, 1000 + b, codes[b])
+        sv.wait()
+        c = codes.cpu().numpy()
+        assert (c[0] == 0).all() and (c[2] == 0).all()
+        assert [i for i in range(n) if c[1, i] != 0] == [9] and c[1, 9] == 5
+    finally:
+        dist.destroy_process_group()
