@@ -537,6 +537,8 @@ struct ovh_ctx {
   // on fstream while batch k + 1's per-vote stages run on stream; OVH_BATCH_SLOTS slots of batch
   // state rotate (a slot is reused only after its final-stream work finished).
   hipStream_t fstream = nullptr;
+  hipStream_t hstream = nullptr;  // hash_to_field of the next batch, beside the current vote
+  hipEvent_t ev_h[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   uint32_t* state_slot[OVH_BATCH_SLOTS] = {};
   uint32_t* red_slot[OVH_BATCH_SLOTS] = {};
@@ -665,6 +667,7 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
   while (cap < n) cap <<= 1;
   HIPCHK(hipStreamSynchronize(c->stream));
   if (c->fstream) HIPCHK(hipStreamSynchronize(c->fstream));
+  if (c->hstream) HIPCHK(hipStreamSynchronize(c->hstream));
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
     if (c->state_slot[k]) (void)hipFree(c->state_slot[k]);
     if (c->red_slot[k]) (void)hipFree(c->red_slot[k]);
@@ -743,12 +746,14 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
     if (hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) != hipSuccess) {
       ovh_destroy(c);
       return nullptr;
     }
     for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
       if (hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c->ev_h[k], hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&c->ev_back[k], hipEventDisableTiming) != hipSuccess) {
         ovh_destroy(c);
         return nullptr;
@@ -768,6 +773,7 @@ void ovh_destroy(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->fstream) (void)hipStreamSynchronize(c->fstream);
+  if (c->hstream) (void)hipStreamSynchronize(c->hstream);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k]})
       if (p) (void)hipFree(p);
@@ -775,8 +781,10 @@ void ovh_destroy(ovh_ctx* c) {
                   (void*)c->result, (void*)c->vm_consts, (void*)c->fin})
     if (p) (void)hipFree(p);
   if (c->fstream) (void)hipStreamDestroy(c->fstream);
+  if (c->hstream) (void)hipStreamDestroy(c->hstream);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
     if (c->ev_front[k]) (void)hipEventDestroy(c->ev_front[k]);
+    if (c->ev_h[k]) (void)hipEventDestroy(c->ev_h[k]);
     if (c->ev_back[k]) (void)hipEventDestroy(c->ev_back[k]);
   }
   for (void* p : c->vm_bufs) (void)hipFree(p);
@@ -1042,13 +1050,27 @@ int ovh_verify_aggregated(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, co
 // level 0 fused in: *outF / *outS = ceil(n / 4) partials as planes in the slot's fold scratch
 // (half 0), *out_m their count.
 static int batch_front(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
-                       uint64_t seed, int32_t* d_codes, Slab* outF, Slab* outS, uint32_t* out_m) {
+                       uint64_t seed, int32_t* d_codes, Slab* outF, Slab* outS, uint32_t* out_m, int slot = -1) {
   Slab s{c->state, c->cap};
   hipStream_t st = c->stream;
   c->ev_mask = 0;
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
   Slab p0{c->red, c->red_cap};
-  { StageScope p(c, ST_H2F); k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s); }
+  if (slot >= 0) {
+    // pipelined: hash_to_field on its own stream, as soon as the slot's previous batch has
+    // finished its per-vote stages (the only reader of the S_U planes), so it runs beside the
+    // current vote kernel; the vote waits for it
+    HIPCHK(hipStreamWaitEvent(c->hstream, c->ev_front[slot], 0));
+    {
+      StageScope p(c, ST_H2F, c->hstream);
+      k_h2f<<<nblk(n), WG, 0, c->hstream>>>(n, d_hashes, c->xmd, s);
+    }
+    HIPCHK(hipEventRecord(c->ev_h[slot], c->hstream));
+    HIPCHK(hipStreamWaitEvent(st, c->ev_h[slot], 0));
+  } else {
+    StageScope p(c, ST_H2F);
+    k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s);
+  }
   {
     StageScope p(c, ST_VOTE);
     k_vm_vote<<<nwg, 64, LDS_VOTE, st>>>(n, c->vm_vote, c->vm_fold, c->vm_consts, d_pks, d_sigs, s, seed, d_codes,
@@ -1239,7 +1261,7 @@ int ovh_verify_batch_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, c
   if (take_slot(c, slot)) return OVH_ERR_DEVICE;
   Slab F, S;
   uint32_t m;
-  int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m);
+  int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m, slot);
   if (e) return e;
   // fold levels: the wide ones on the main stream (short, high priority), the narrow ones and
   // the combined check + fallback on the final stream -- balancing the two streams' chains
@@ -1262,6 +1284,7 @@ int ovh_batch_wait(ovh_ctx* c) {
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->fstream));
+  HIPCHK(hipStreamSynchronize(c->hstream));
   return 0;
 }
 
