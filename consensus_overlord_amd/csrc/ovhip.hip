@@ -164,7 +164,8 @@ struct VmDev {  // a program in device memory
   uint64_t* trace;  // OVH_FLAG_VM_TRACE: nphases + 1 timestamps of workgroup 0, else null
 };
 
-#define VM_SLICES 4  // 16-lane slices per 64-lane workgroup
+#define VM_SLICES 4  // 16-lane slices per 64-lane workgroup (vote, pairchk)
+#define VM_FOLD_UNITS (64 / VM_FOLD_W)  // fold units per 64-lane workgroup
 
 __device__ __forceinline__ void load_consts(uint32_t* cst, const uint32_t* __restrict__ g, uint32_t n) {
   for (uint32_t k = threadIdx.x; k < n * 12; k += blockDim.x) cst[k] = g[k];
@@ -578,15 +579,14 @@ static const char* const STAGE_NAMES[OVH_NSTAGES] = {"hash_to_field", "vote", "f
 
 // LDS bytes of the VM kernels: constants + slices x slots (+ a 16-byte slice header for vote)
 static constexpr size_t LDS_VOTE = (size_t)VM_NCONST * 48 + VM_SLICES * ((size_t)VM_VOTE_NSLOTS * 48 + 16);
-static constexpr size_t LDS_FOLD = (size_t)VM_NCONST * 48 + VM_SLICES * (size_t)VM_FOLD_NSLOTS * 48;
+static constexpr size_t LDS_FOLD = (size_t)VM_NCONST * 48 + VM_FOLD_UNITS * (size_t)VM_FOLD_NSLOTS * 48;
 static constexpr size_t LDS_FINAL = (size_t)VM_NCONST * 48 + (size_t)VM_FINAL_NSLOTS * 48;
 static constexpr size_t LDS_PAIRCHK = (size_t)VM_NCONST * 48 + VM_SLICES * (size_t)VM_PAIRCHK_NSLOTS * 48;
-static_assert(VM_VOTE_W * VM_SLICES == 64 && VM_FOLD_W * VM_SLICES == 64 && VM_PAIRCHK_W * VM_SLICES == 64 &&
+static_assert(VM_VOTE_W * VM_SLICES == 64 && VM_FOLD_W * VM_FOLD_UNITS == 64 && VM_PAIRCHK_W * VM_SLICES == 64 &&
                   VM_FINAL_W == 64, "VM slice widths");
 static constexpr size_t LDS_FOLD1 = (size_t)VM_NCONST * 48 + (size_t)VM_FOLD_NSLOTS * 48;
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
 static_assert(VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_NSLOTS * 12 + 4), "fused fold reuses the vote slots");
-static_assert(VM_FOLD_W == VM_VOTE_W, "fused fold slice width");
 
 static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphases, uint32_t W, const uint16_t* in,
                      uint32_t nin, const uint16_t* out, uint32_t nout) {
@@ -630,7 +630,7 @@ static int vm_init(ovh_ctx* c) {
                 VM_PAIRCHK_NIN, VM_PAIRCHK_OUT, VM_PAIRCHK_NOUT))
     return OVH_ERR_DEVICE;
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE));
-  HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold<VM_SLICES>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold<VM_FOLD_UNITS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)LDS_FOLD));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FOLD1));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FINAL));
@@ -1099,7 +1099,7 @@ static int fold_levels(ovh_ctx* c, hipStream_t st, int slices, Slab* F, Slab* S,
     if (slices == 1)
       k_vm_fold<1><<<mo, 64, LDS_FOLD1, st>>>(*m, c->vm_fold, c->vm_consts, *F, *S, o, nullptr);
     else
-      k_vm_fold<VM_SLICES><<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, st>>>(*m, c->vm_fold, c->vm_consts, *F,
+      k_vm_fold<VM_FOLD_UNITS><<<(mo + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(*m, c->vm_fold, c->vm_consts, *F,
                                                                                  *S, o, nullptr);
     *F = o;
     *S = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
@@ -1139,7 +1139,7 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   if (m > 1) {  // fold the last <= 4 into one partial
     uint32_t* base = c->red + (size_t)(F.p == c->red ? 1 : 0) * PART_PLANES * 12 * c->red_cap;
     Slab o{base, c->red_cap};
-    k_vm_fold<VM_SLICES><<<1, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o, nullptr);
+    k_vm_fold<VM_FOLD_UNITS><<<1, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o, nullptr);
     F = o;
   }
   // pack element 0 (F planes, S planes) into the AoS partial
@@ -1179,7 +1179,7 @@ static int stage_partials(ovh_ctx* c, hipStream_t st, size_t k, const uint8_t* d
   } else {
     uint32_t* o = scratch + (size_t)PART_PLANES * 12 * 16;
     Slab oF{o, 4};
-    k_vm_fold<VM_SLICES><<<1, 64, LDS_FOLD, st>>>((uint32_t)k, c->vm_fold, c->vm_consts, uF, uS, oF, nullptr);
+    k_vm_fold<VM_FOLD_UNITS><<<1, 64, LDS_FOLD, st>>>((uint32_t)k, c->vm_fold, c->vm_consts, uF, uS, oF, nullptr);
     *F = oF;
     *S = Slab{o + (size_t)12 * 12 * 4, 4};
     *m = (uint32_t)((k + 3) / 4);
@@ -1203,7 +1203,7 @@ int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials)
     const uint32_t mo = (m + 3) / 4;
     uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
     Slab o{base, c->red_cap};
-    k_vm_fold<VM_SLICES><<<(mo + VM_SLICES - 1) / VM_SLICES, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts,
+    k_vm_fold<VM_FOLD_UNITS><<<(mo + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts,
                                                                                        F, S, o, nullptr);
     F = o;
     S = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};

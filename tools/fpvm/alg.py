@@ -784,15 +784,15 @@ class Alg:
         return (X, Y, Z)
 
     def clear_cofactor(self, A):
-        """h_eff A = [x^2 - x - 1] A + [x - 1] psi(A) + psi^2(2A), x = -X_ABS:
-        = t2 + t1 - A - psi(t1 + A) + psi^2(2A) with t1 = [X_ABS] A, t2 = [X_ABS] t1."""
+        """h_eff A = [x^2 - x - 1] A + [x - 1] psi(A) + psi^2(2A), x = -X_ABS (RFC 9380 G.3).
+        With t1 = [X_ABS] A and psi commuting with scalars:
+          h_eff A = [X_ABS] B + K,  B = t1 - psi(A),  K = B - A + psi^2(2A),
+        so only K (one point) is held across the second scalar chain."""
         t1 = self.pt_mul_fixed("f2", A, X_ABS)
-        t2 = self.pt_mul_fixed("f2", t1, X_ABS)
-        acc = self.pt_add("f2", t2, t1)
-        acc = self.pt_add("f2", acc, self.pt_neg("f2", A))
-        acc = self.pt_add("f2", acc, self.pt_neg("f2", self.g2_psi(self.pt_add("f2", t1, A))))
-        acc = self.pt_add("f2", acc, self.g2_psi(self.g2_psi(self.pt_dbl("f2", A))))
-        return acc
+        B = self.pt_add("f2", t1, self.pt_neg("f2", self.g2_psi(A)))
+        K = self.pt_add("f2", self.pt_add("f2", B, self.pt_neg("f2", A)),
+                        self.g2_psi(self.g2_psi(self.pt_dbl("f2", A))))
+        return self.pt_add("f2", self.pt_mul_fixed("f2", B, X_ABS), K)
 
     def hash_to_g2(self, u0, u1):
         q0 = self.iso_map(*self.map_to_curve_sswu(u0))
