@@ -213,6 +213,15 @@ def main():
         dom = max((k for k in range(nst) if names[k] in STAGE_TO_WORK), key=lambda k: avg_ms[k])
         dname = names[dom]
         units = 1 if dname in PER_BATCH_STAGES else B
+        # HBM bytes per launch of the dominant kernel from the committed PMC pass
+        # (tools/pmc_round.sh; FETCH_SIZE doubled per the gfx950 correction); null if absent
+        traffic = None
+        tpath = os.path.join(ROOT, "consensus_overlord_amd", "pmc_traffic.json")
+        if os.path.exists(tpath):
+            with open(tpath) as fh:
+                tk = json.load(fh)["kernels"].get("k_vm_" + dname)
+            if tk is not None and B == 4096:
+                traffic = tk["hbm_bytes_per_launch"]
         macs = Mu[STAGE_TO_WORK[dname]] * units * macs_per_M
         achieved = macs / (avg_ms[dom] * 1e-3) / 1e12
         value = world * B * args.steps / elapsed
@@ -242,7 +251,8 @@ def main():
                 "unit": "TOP/s (32x32-bit integer MAC lane-ops; peak = measured v_mad_u64_u32 rate)",
                 "frac": round(achieved * 1e12 / PEAK_MAD_U64, 4),
                 "frac_of_fullrate_valu": round(achieved * 1e12 / PEAK_FULLRATE, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x 2 + WRITE_SIZE, pmc_traffic.json)",
                 "path_M_per_vote": round(path_M, 1),
                 "path_frac": round(value / world * path_M * macs_per_M / PEAK_MAD_U64, 4),
             },
