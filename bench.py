@@ -39,6 +39,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 SEED = 0xC17A
+G2_GEN_COMPRESSED = bytes.fromhex(
+    "93e02b6052719f607dacd3a088274f65596bd0d09920b61ab5da61bbdc7f5049334cf11213945d57e5ac7d055d042b7e"
+    "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8")
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 OVH_FLAG_PROFILE = 0x2
 # measured v_mad_u64_u32 lane-op rate on gfx950 (tools/ubench/int_rates.hip,
@@ -46,6 +49,7 @@ OVH_FLAG_PROFILE = 0x2
 # (256 CU x 4 SIMD x 32 lanes x 2.4 GHz).
 PEAK_MAD_U64 = 2.9143e13
 PEAK_FULLRATE = 256 * 4 * 32 * 2.4e9
+W_V_CANON = 18300   # algorithmic Montgomery products per verification
 STAGE_TO_WORK = {"hash_to_field": "hash_to_field", "vote": "vote", "fold": "fold_per_partial",
                  "final": "final_per_batch", "fallback": "fallback"}
 PER_BATCH_STAGES = {"final"}
@@ -92,12 +96,99 @@ def cpu_baseline(sigs: np.ndarray, hs: np.ndarray, pks: np.ndarray, budget_s: fl
             raise RuntimeError("CPU oracle rejects GPU-made votes")
         n1 += chunk
     dt_1 = time.perf_counter() - t0
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), None)
+    except OSError:
+        pass
     return {"value": round(len(sigs) / dt_b, 2), "unit": "verifications/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpus": os.cpu_count(),
             "sample": "all %d votes of the workload, RLC batch verify on %d threads (C restatement "
                       "oracle/c/bls_oracle.c, not blst), %.2f s" % (len(sigs), threads, dt_b),
             "serial_1core": {"value": round(n1 / dt_1, 2), "cores": 1,
                              "sample": "first %d votes, per-vote verify_signature serially (the reference's "
                                        "call shape), %.2f s" % (n1, dt_1)}}
+
+
+def latencies(ctx, sigs, hs, pks) -> dict:
+    """Untimed latency probes after the throughput run (configs 2 and 5 report
+    latency; the reference's own call shape is one verify_signature per vote):
+      verify_ms      one ovh_verify (Crypto::verify_signature) of a valid vote, median of 5
+      qc67_ms        config 2: verify_aggregated_signature over 67 voters, median of 3
+      qc_table_ms    config 2 through the validator table (ovh_verify_qc_batch, one QC)
+      cfg5_ms        config 5: 1024 votes with 1% sigma + G2, batch incl. bisection, median of 3
+      cfg5_valid_ms  the same 1024 votes all valid (no bisection)"""
+    import torch
+    from consensus_overlord_amd import device as dev
+    lib = ctx.lib
+    out = {}
+    s0, h0, p0 = (bytes(x[0].cpu().numpy()) for x in (sigs, hs, pks))
+
+    def med(fn, k):
+        ts = []
+        for _ in range(k):
+            t = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t)
+        return round(float(np.median(ts)) * 1e3, 3)
+    assert lib.ovh_verify(ctx.ptr, s0, 96, h0, 32, p0, 48) == 0
+    out["verify_ms"] = med(lambda: lib.ovh_verify(ctx.ptr, s0, 96, h0, 32, p0, 48), 5)
+    # config 2: 67 of 100 validators sign one vote digest; aggregate made with the library
+    n = 67
+    digest = h0
+    sks = torch.from_numpy(np.stack([np.frombuffer(
+        (int.from_bytes(hashlib.sha256(b"cfg2" + i.to_bytes(4, "big")).digest(), "big") % R_ORDER or 1)
+        .to_bytes(32, "big"), dtype=np.uint8) for i in range(100)])).cuda()
+    qp = dev.sk_to_pk_batch(ctx, sks).cpu().numpy()
+    qs = dev.sign_batch(ctx, sks[:n], torch.from_numpy(np.tile(np.frombuffer(digest, dtype=np.uint8), (n, 1))).cuda())
+    qs = qs.cpu().numpy()
+    lens = (ctypes.c_size_t * n)(*([96] * n))
+    plen = (ctypes.c_size_t * n)(*([48] * n))
+    agg = ctypes.create_string_buffer(96)
+    assert lib.ovh_aggregate_sigs(ctx.ptr, qs.tobytes(), lens, n, qp[:n].tobytes(), plen, n, agg) == 0
+    out["aggregate67_ms"] = med(lambda: lib.ovh_aggregate_sigs(ctx.ptr, qs.tobytes(), lens, n, qp[:n].tobytes(),
+                                                               plen, n, agg), 3)
+    assert lib.ovh_verify_aggregated(ctx.ptr, agg.raw, 96, digest, 32, qp[:n].tobytes(), plen, n) == 0
+    out["qc67_ms"] = med(lambda: lib.ovh_verify_aggregated(ctx.ptr, agg.raw, 96, digest, 32, qp[:n].tobytes(),
+                                                           plen, n), 3)
+    assert lib.ovh_set_validators(ctx.ptr, qp.tobytes(), 100) == 0
+    order = sorted(range(100), key=lambda i: bytes(qp[i]))
+    bm = bytearray(13)
+    for pos, i in enumerate(order):
+        if i < n:
+            bm[pos // 8] |= 0x80 >> (pos % 8)
+    qcode = (ctypes.c_int32 * 1)()
+    assert lib.ovh_verify_qc_batch(ctx.ptr, 1, agg.raw, digest, bytes(bm), 13, qcode) == 0 and qcode[0] == 0
+    out["qc_table_ms"] = med(lambda: lib.ovh_verify_qc_batch(ctx.ptr, 1, agg.raw, digest, bytes(bm), 13, qcode), 3)
+    assert lib.ovh_set_validators(ctx.ptr, None, 0) == 0
+    # config 5: 1024 votes, 1% sigma + G2 at seeded positions
+    import random
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "py"))
+    m = 1024
+    s_h = sigs[:m].cpu().numpy().copy()
+    bad = sorted(random.Random(5).sample(range(m), m // 100))
+    g2 = G2_GEN_COMPRESSED
+    for i in bad:   # sigma + G2 via the library: aggregate(sigma_i, G2) (its voters are only parsed)
+        a = ctypes.create_string_buffer(96)
+        two = (ctypes.c_size_t * 2)(96, 96)
+        pl2 = (ctypes.c_size_t * 2)(48, 48)
+        assert lib.ovh_aggregate_sigs(ctx.ptr, bytes(s_h[i]) + g2, two, 2, p0 + p0, pl2, 2, a) == 0
+        s_h[i] = np.frombuffer(a.raw, dtype=np.uint8)
+    d5 = torch.from_numpy(s_h).cuda()
+    c5 = torch.empty((m,), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+
+    def cfg5(sg):
+        dev.verify_batch(ctx, sg, hs[:m], pks[:m], c5)
+    cfg5(d5)
+    flagged = [i for i in range(m) if int(c5[i].item()) != 0]
+    if flagged != bad:
+        raise RuntimeError("config 5: flagged %s, expected %s" % (flagged[:8], bad[:8]))
+    out["cfg5_ms"] = med(lambda: cfg5(d5), 3)
+    out["cfg5_valid_ms"] = med(lambda: cfg5(sigs[:m]), 3)
+    out["cfg5_verifs_per_s"] = round(m / (out["cfg5_ms"] * 1e-3), 1)
+    return out
 
 
 def main():
@@ -111,6 +202,7 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=3, help="untimed unpipelined batches for stage times")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latency", action="store_true", help="skip the untimed latency probes")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -155,13 +247,13 @@ def main():
             dev.batch_wait(ctx)
 
     def step(s: int) -> None:
-        """Enqueue batch s. Pipelined: batch s's combined check / fallback (second stream) overlaps
-        batch s + 1's per-vote stages; every batch's codes row is final after batch_wait."""
-        seed = (SEED << 32) ^ (s * 0x10001)
+        """Enqueue batch s. Pipelined: batch s's combined check / bisection (second stream)
+        overlaps batch s + 1's per-vote stages; every batch's codes row is final after
+        batch_wait. Each batch's RLC coefficients come from a fresh getrandom seed (library)."""
         if world == 1:
-            dev.verify_batch_async(ctx, sigs, hs, pks, seed, codes[s])
+            dev.verify_batch_async(ctx, sigs, hs, pks, codes[s])
         else:
-            shards.submit(s, sigs, hs, pks, seed, codes[s])
+            shards.submit(s, sigs, hs, pks, codes[s], index_base=rank * B)
 
     for s in range(args.warmup):
         step(s)
@@ -222,10 +314,16 @@ def main():
                 tk = json.load(fh)["kernels"].get("k_vm_" + dname)
             if tk is not None and B == 4096:
                 traffic = tk["hbm_bytes_per_launch"]
-        macs = Mu[STAGE_TO_WORK[dname]] * units * macs_per_M
+        # algorithmic work of the dominant stage: SURVEY.md 8(d) canonical W_v = 18,300 M per vote
+        # (Appendix C) less the Fp12 merge (54 M) and the amortised final exponentiation (4 M),
+        # which other kernels do; the program's own count (vote program) is reported beside it
+        canon = {"vote": W_V_CANON - 54 - 4}
+        work_M = canon.get(dname, Mu[STAGE_TO_WORK[dname]])
+        macs = work_M * units * macs_per_M
         achieved = macs / (avg_ms[dom] * 1e-3) / 1e12
+        prog_achieved = Mu[STAGE_TO_WORK[dname]] * units * macs_per_M / (avg_ms[dom] * 1e-3) / 1e12
         value = world * B * args.steps / elapsed
-        path_M = Mu["hash_to_field"] + Mu["vote"] + Mu["fold_per_partial"] * 4.0 / 3.0 + Mu["final_per_batch"] / B
+        path_M = W_V_CANON
         line = {
             "metric": "BLS12-381 vote verifications/sec (batch 4096) at 1/2/4/8 MI355X vs host blst",
             "value": round(value, 2),
@@ -251,6 +349,11 @@ def main():
                 "unit": "TOP/s (32x32-bit integer MAC lane-ops; peak = measured v_mad_u64_u32 rate)",
                 "frac": round(achieved * 1e12 / PEAK_MAD_U64, 4),
                 "frac_of_fullrate_valu": round(achieved * 1e12 / PEAK_FULLRATE, 4),
+                "work_M_per_unit": work_M,
+                "work_basis": "SURVEY 8(d) canonical W_v minus merge + amortised FE" if dname in canon
+                              else "program heavy ops (workmodel.json)",
+                "program_M_per_unit": Mu[STAGE_TO_WORK[dname]],
+                "program_frac": round(prog_achieved * 1e12 / PEAK_MAD_U64, 4),
                 "traffic": traffic,
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x 2 + WRITE_SIZE, pmc_traffic.json)",
                 "path_M_per_vote": round(path_M, 1),
@@ -258,9 +361,11 @@ def main():
             },
             "stage_ms": stages,
             "batch_latency_ms": round(float(np.median(lat)) * 1e3, 3) if lat else None,
-            "pipelined": "batch k's combined check + fallback (second stream) overlap batch k+1's per-vote "
+            "pipelined": "batch k's combined check + bisection (second stream) overlap batch k+1's per-vote "
                          "stages; all %d timed batches complete inside the timed region" % args.steps,
         }
+        if world == 1 and not args.no_latency:
+            line["latency"] = latencies(ctx, sigs, hs, pks)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(sigs.cpu().numpy(), hs_h, pks.cpu().numpy(), args.cpu_seconds)
         print(json.dumps(line), flush=True)

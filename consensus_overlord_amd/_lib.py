@@ -16,23 +16,32 @@ _vp = ctypes.c_void_p
 # (name, restype, argtypes) -- mirrors include/ovhip.h
 SIGNATURES = [
     ("ovh_create", _vp, [ctypes.c_int, _u8p, _sz, ctypes.c_uint32]),
+    ("ovh_create_multi", _vp, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, _u8p, _sz, ctypes.c_uint32]),
     ("ovh_destroy", None, [_vp]),
+    ("ovh_device_count", ctypes.c_int, [_vp]),
     ("ovh_stream", _vp, [_vp]),
     ("ovh_sm3", ctypes.c_int, [_u8p, _sz, _u8p]),
+    ("ovh_sk_parse", ctypes.c_int, [_vp, _u8p, _sz, _u8p]),
     ("ovh_sign", ctypes.c_int, [_vp, _u8p, _sz, _u8p, _sz, _u8p]),
     ("ovh_sk_to_pk", ctypes.c_int, [_vp, _u8p, _sz, _u8p]),
     ("ovh_verify", ctypes.c_int, [_vp, _u8p, _sz, _u8p, _sz, _u8p, _sz]),
     ("ovh_aggregate_sigs", ctypes.c_int, [_vp, _u8p, _szp, _sz, _u8p, _szp, _sz, _u8p]),
     ("ovh_aggregate_pks", ctypes.c_int, [_vp, _u8p, _szp, _sz, _u8p]),
     ("ovh_verify_aggregated", ctypes.c_int, [_vp, _u8p, _sz, _u8p, _sz, _u8p, _szp, _sz]),
-    ("ovh_verify_batch", ctypes.c_int, [_vp, _sz, _u8p, _u8p, _u8p, ctypes.c_uint64, _vp]),
-    ("ovh_verify_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
-    ("ovh_batch_partial_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp]),
-    ("ovh_combine_partials_device", ctypes.c_int, [_vp, _sz, _vp]),
+    ("ovh_set_validators", ctypes.c_int, [_vp, _u8p, _sz]),
+    ("ovh_verify_batch", ctypes.c_int, [_vp, _sz, _u8p, _u8p, _u8p, _vp]),
+    ("ovh_prefetch", ctypes.c_int, [_vp, _sz, _u8p, _u8p, _u8p]),
+    ("ovh_cache_config", ctypes.c_int, [_vp, _sz]),
+    ("ovh_cache_stats", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
+    ("ovh_verify_qc_batch", ctypes.c_int, [_vp, _sz, _u8p, _u8p, _u8p, _sz, _vp]),
+    ("ovh_set_test_rlc", ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64]),
+    ("ovh_verify_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp]),
+    ("ovh_batch_partial_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("ovh_combine_partials_device", ctypes.c_int, [_vp, _sz, _vp, ctypes.POINTER(ctypes.c_int32)]),
     ("ovh_batch_fallback_device", ctypes.c_int, [_vp, _sz, _vp]),
-    ("ovh_verify_batch_device_async", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, ctypes.c_uint64, _vp]),
+    ("ovh_verify_batch_device_async", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp]),
     ("ovh_batch_wait", ctypes.c_int, [_vp]),
-    ("ovh_combine_partials_device_async", ctypes.c_int, [_vp, _sz, _vp, _sz, _vp]),
+    ("ovh_combine_partials_device_async", ctypes.c_int, [_vp, _sz, _vp, _sz, _vp, _vp]),
     ("ovh_stage_times", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_float), _sz]),
     ("ovh_stage_name", ctypes.c_char_p, [ctypes.c_int]),
     ("ovh_vm_trace", ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), _sz]),

@@ -21,6 +21,14 @@ ERR_LEN_MISMATCH = 101
 ERR_PUBKEY = 102
 ERR_ARG = 103
 ERR_DEVICE = 200
+ERR_RNG = 201
+
+# include/ovhip.h context flags
+FLAG_AGG_NO_GROUPCHECK = 0x1
+FLAG_PROFILE = 0x2
+FLAG_VM_TRACE = 0x4
+FLAG_TEST_RLC = 0x8     # tests only: predictable batch coefficients (Context.set_test_rlc)
+FLAG_SK_RAW = 0x10      # private key = raw scalar 0 < sk < r instead of IETF KeyGen
 
 BLST_ERRORS = {
     1: "BLST_BAD_ENCODING",
@@ -76,15 +84,31 @@ def _concat(items: Sequence[bytes]):
 
 
 class Context:
-    """One libovhip context (device memory, stream, DST) on HIP device `device`."""
+    """One libovhip context (device memory, streams, DST) on HIP device `device`, or over
+    several devices of this process (`devices=[...]`, ovh_create_multi)."""
 
-    def __init__(self, device: int = 0, dst: Optional[bytes] = None, flags: int = 0):
+    def __init__(self, device: int = 0, dst: Optional[bytes] = None, flags: int = 0,
+                 devices: Optional[Sequence[int]] = None):
         self.lib = _lib.load()
         d = None if dst is None else bytes(dst)
-        self.ptr = self.lib.ovh_create(device, d, 0 if d is None else len(d), flags)
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            self.ptr = self.lib.ovh_create_multi(arr, len(devices), d, 0 if d is None else len(d), flags)
+            device = devices[0]
+        else:
+            self.ptr = self.lib.ovh_create(device, d, 0 if d is None else len(d), flags)
         if not self.ptr:
             raise DeviceError("ovh_create failed on device %d (no usable MI355X?)" % device)
         self.device = device
+        self.flags = flags
+
+    @property
+    def device_count(self) -> int:
+        return self.lib.ovh_device_count(self.ptr)
+
+    def set_test_rlc(self, seed: int, index_base: int = 0) -> None:
+        """Tests only (context made with FLAG_TEST_RLC): reproducible batch coefficients."""
+        raise_for(self.lib.ovh_set_test_rlc(self.ptr, seed & 0xFFFFFFFFFFFFFFFF, index_base))
 
     def close(self):
         if getattr(self, "ptr", None):
@@ -106,8 +130,9 @@ class ConsensusCrypto:
     """Mirror of `ConsensusCrypto` / overlord's `Crypto` trait (consensus.rs:339-463)."""
 
     def __init__(self, private_key: bytes, device: int = 0, dst: Optional[bytes] = None, ctx: Optional[Context] = None):
-        """consensus.rs:347-359 `new`: private key = 32-byte scalar (hex text or raw bytes);
-        name = the 48-byte compressed public key; common_ref = ''."""
+        """consensus.rs:347-359 `new`: the private key file's bytes (hex text or raw bytes),
+        parsed as ophelia-blst's BlsPrivateKey::try_from (IETF KeyGen by default, see
+        ovh_sk_parse); name = the 48-byte compressed public key; common_ref = ''."""
         if isinstance(private_key, str):
             private_key = bytes.fromhex(private_key.strip())
         self.ctx = ctx if ctx is not None else Context(device, dst)
@@ -125,8 +150,19 @@ class ConsensusCrypto:
             return cls(bytes.fromhex(fh.read().strip()), **kw)
 
     def update_pubkeys(self, new_pubkeys: Sequence[bytes]) -> None:
-        """consensus.rs:361-363."""
-        self.pubkeys = [bytes(p) for p in new_pubkeys]
+        """consensus.rs:361-363 (callers :131-136, :622-629): the validator keys, 48-byte
+        compressed, in config order -> the device validator table (ovh_set_validators)."""
+        keys = [bytes(p) for p in new_pubkeys]
+        if any(len(k) != 48 for k in keys):
+            raise Other("lose public key")
+        self.pubkeys = keys
+        raise_for(self.lib.ovh_set_validators(self.ctx.ptr, b"".join(keys), len(keys)))
+
+    def scalar(self) -> bytes:
+        """The 32-byte scalar the private key parses to (ovh_sk_parse)."""
+        out = ctypes.create_string_buffer(32)
+        raise_for(self.lib.ovh_sk_parse(self.ctx.ptr, self.private_key, len(self.private_key), out))
+        return out.raw
 
     # ---- overlord::Crypto ----
     def hash(self, msg: bytes) -> bytes:
@@ -170,9 +206,8 @@ class ConsensusCrypto:
         raise_for(self.lib.ovh_aggregate_pks(self.ctx.ptr, vd, vl, len(voters), out))
         return out.raw
 
-    def verify_batch(self, signatures, hashes, voters, seed: int = 0) -> np.ndarray:
-        """Batched verify_signature: returns int32 codes[n], codes[i] == the ovh_verify result
-        for vote i (0 = Ok). Fixed-size inputs: 96-byte sigs, 32-byte hashes, 48-byte pks."""
+    @staticmethod
+    def _fixed(signatures, hashes, voters):
         n = len(signatures)
         if not (len(hashes) == len(voters) == n):
             raise ValueError("batch lists must have equal length")
@@ -180,8 +215,44 @@ class ConsensusCrypto:
         hs = b"".join(bytes(h) for h in hashes)
         pk = b"".join(bytes(v) for v in voters)
         if len(sig) != 96 * n or len(hs) != 32 * n or len(pk) != 48 * n:
-            raise ValueError("verify_batch takes 96-byte signatures, 32-byte hashes, 48-byte voters")
+            raise ValueError("batches take 96-byte signatures, 32-byte hashes, 48-byte voters")
+        return n, sig, hs, pk
+
+    def verify_batch(self, signatures, hashes, voters) -> np.ndarray:
+        """Batched verify_signature: returns int32 codes[n], codes[i] == the ovh_verify result
+        for vote i (0 = Ok). Fixed-size inputs: 96-byte sigs, 32-byte hashes, 48-byte pks."""
+        n, sig, hs, pk = self._fixed(signatures, hashes, voters)
         codes = np.zeros(max(n, 1), dtype=np.int32)
-        raise_for(self.lib.ovh_verify_batch(self.ctx.ptr, n, sig, hs, pk, seed & 0xFFFFFFFFFFFFFFFF,
-                                            codes.ctypes.data_as(ctypes.c_void_p)))
+        raise_for(self.lib.ovh_verify_batch(self.ctx.ptr, n, sig, hs, pk, codes.ctypes.data_as(ctypes.c_void_p)))
+        return codes[:n]
+
+    def prefetch(self, signatures, hashes, voters) -> None:
+        """Vote-batching ingress (ovh_prefetch): batch-verify the votes now; later
+        verify_signature calls on the same bytes are answered from the context's cache."""
+        n, sig, hs, pk = self._fixed(signatures, hashes, voters)
+        raise_for(self.lib.ovh_prefetch(self.ctx.ptr, n, sig, hs, pk))
+
+    def cache_stats(self):
+        """(hits, misses, entries) of the verdict cache."""
+        st = (ctypes.c_uint64 * 3)()
+        raise_for(self.lib.ovh_cache_stats(self.ctx.ptr, st))
+        return tuple(int(x) for x in st)
+
+    def verify_qc_batch(self, signatures, hashes, bitmaps) -> np.ndarray:
+        """Batched QC check (ovh_verify_qc_batch): QC j signed by the validators (update_pubkeys)
+        selected by bitmaps[j] over the key-sorted validator list; codes[j] equals
+        verify_aggregated_signature(signatures[j], hashes[j], those voters)."""
+        n = len(signatures)
+        if not (len(hashes) == len(bitmaps) == n):
+            raise ValueError("QC lists must have equal length")
+        bl = len(bitmaps[0]) if n else 0
+        if any(len(b) != bl for b in bitmaps):
+            raise ValueError("bitmaps must have equal length")
+        sig = b"".join(bytes(s) for s in signatures)
+        hs = b"".join(bytes(h) for h in hashes)
+        if len(sig) != 96 * n or len(hs) != 32 * n:
+            raise ValueError("QC batches take 96-byte signatures and 32-byte hashes")
+        codes = np.zeros(max(n, 1), dtype=np.int32)
+        raise_for(self.lib.ovh_verify_qc_batch(self.ctx.ptr, n, sig, hs, b"".join(bytes(b) for b in bitmaps), bl,
+                                               codes.ctypes.data_as(ctypes.c_void_p)))
         return codes[:n]

@@ -5,22 +5,36 @@
 //   k_vm_vote     16-lane slice per vote, 4 votes per wave: the Fp-VM "vote" program --
 //                 pk / sig decompression + subgroup checks, hash_to_G2, r pk, r sigma,
 //                 f = Miller(r pk, H); the epilogue writes the vote's code with the reference
-//                 precedence and its (f, r sigma) contribution (identity if the vote failed)
-//   k_vm_fold     16-lane slice per 4 partials: (prod f, sum S), repeated down to <= 4
+//                 precedence and its (f, r sigma) contribution (identity if the vote failed),
+//                 then folds the workgroup's 4 votes into one partial (level 0)
+//   k_vm_vote_t   the same with the public key from the device validator table (or a QC's
+//                 aggregated key): no decompression / subgroup check of the key
+//   k_vm_fold     fold levels: 4 partials -> (prod f, sum S); level 1 = groups of 16 votes
 //   k_vm_final    one wave: prod f * Miller(-G1, sum S) -> final exponentiation == 1 ?
-//   k_vm_pairchk  16-lane slice per surviving vote when the combined check fails
+//   k_vm_group    bisection, when the combined check failed: the same check per 16-vote group
+//   k_vm_votechk  bisection, per vote of a failing group: f_i * Miller(-G1, r_i sigma_i) == 1
 // Per-vote state lives in HBM as structure-of-arrays by limb: limb k of element i of an Fp
 // plane j at slab[(j * 12 + k) * cap + i].
 #include <hip/hip_runtime.h>
 
+#include <errno.h>
+#include <sys/random.h>
+#include <sys/types.h>
+
+#include <algorithm>
+#include <atomic>
+#include <deque>
 #include <mutex>
 #include <new>
+#include <string>
 #include <string.h>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/ovhip.h"
 #include "bls/verify.hpp"
 #include "fpvm.hpp"
+#include "keygen.hpp"
 #include "sm3.hpp"
 #include "vm_progs.inc"
 
@@ -89,7 +103,6 @@ struct Slab {
 // Fp planes of the per-vote state slab.
 enum : uint32_t {
   S_U = VM_S_U,       // 4 planes: u0, u1 (hash_to_field, Montgomery)
-  S_FB = VM_S_FB,     // 12 planes: pk affine (2), sig affine (4), H projective (6) -- fallback inputs
   S_RS = VM_S_RS,     // 6 planes: r * sig (projective)
   S_F = VM_S_F,       // 12 planes: f = Miller(r pk, H)
   S_TOTAL = VM_S_TOTAL,
@@ -102,9 +115,10 @@ constexpr size_t FIN_STRIDE = (size_t)PART_PLANES * 12 * 20;
 enum : int { ST_H2F = 0, ST_VOTE, ST_FOLD, ST_FINAL, ST_FALLBACK };
 static_assert(ST_FALLBACK + 1 == OVH_NSTAGES, "stage table");
 
-__device__ __forceinline__ uint64_t rlc_scalar(uint64_t seed, uint32_t i) {
-  // SplitMix64 on (seed, i): the 64-bit RLC coefficient of vote i (never 0).
-  uint64_t z = seed + 0x9e3779b97f4a7c15ull * ((uint64_t)i + 1);
+__device__ __forceinline__ uint64_t rlc_scalar(uint64_t seed, uint64_t i) {
+  // SplitMix64 on (seed, i): the 64-bit RLC coefficient of vote i (never 0). The seed is a
+  // fresh secret per batch (getrandom, host side), so the coefficients are unpredictable.
+  uint64_t z = seed + 0x9e3779b97f4a7c15ull * (i + 1);
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   z = z ^ (z >> 31);
@@ -164,7 +178,7 @@ struct VmDev {  // a program in device memory
   uint64_t* trace;  // OVH_FLAG_VM_TRACE: nphases + 1 timestamps of workgroup 0, else null
 };
 
-#define VM_SLICES 4  // 16-lane slices per 64-lane workgroup (vote, pairchk)
+#define VM_SLICES 4  // 16-lane slices per 64-lane workgroup (vote, vote_t)
 #define VM_FOLD_UNITS (64 / VM_FOLD_W)  // fold units per 64-lane workgroup
 
 __device__ __forceinline__ void load_consts(uint32_t* cst, const uint32_t* __restrict__ g, uint32_t n) {
@@ -221,7 +235,8 @@ __device__ __forceinline__ void fold_unit(uint32_t t, uint32_t m, const VmDev& p
 // contribution. LDS: constants, then VM_SLICES x (VM_VOTE_NSLOTS slots).
 __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
                                                 const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
-                                                Slab s, uint64_t seed, int32_t* __restrict__ codes, Slab part0) {
+                                                Slab s, uint64_t seed, uint64_t base, int32_t* __restrict__ codes,
+                                                Slab part0) {
   __builtin_amdgcn_s_setprio(2);  // per-vote stages outrank a co-resident final-stream wave
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
@@ -257,7 +272,7 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
     }
   }
   __syncthreads();
-  vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, i),
+  vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
           vm::Out{s.p, s.cap, i},
           blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) {
@@ -339,28 +354,203 @@ __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const u
   if (lane == 0) *result = slot_flag_get(slots, VM_FINAL_OUT[0]) ? 1 : 0;
 }
 
-// Per-vote fallback: codes[i] (still 0) := e(pk, H) == e(G1, sigma) ? 0 : VERIFY_FAIL.
-__global__ __launch_bounds__(64) void k_vm_pairchk(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g, Slab s,
-                                                   int32_t* __restrict__ codes, const int32_t* __restrict__ verdict) {
-  if (verdict && *verdict == 1) return;  // pipelined path: the combined check passed
+// Public keys given as points (ovh_set_validators table, or a QC's aggregated key): planes
+// X, Y, Z (homogeneous projective, Montgomery) of `cap` entries, plus per-entry flags.
+#define PKF_PARSE 1u  // the 48 bytes did not parse -> "lose public key" (102)
+#define PKF_INF 2u    // the point at infinity      -> BLST_PK_IS_INFINITY (6) at verify
+#define PKF_GRP 4u    // not in G1                  -> BLST_POINT_NOT_IN_GROUP (3) at verify
+struct PkSrc {
+  const uint32_t* planes;
+  uint32_t cap;
+  const uint32_t* flags;
+  const int32_t* idx;  // vote i uses entry idx[i] (null: entry i)
+};
+
+// vote_t: the vote program without the key's decompression / subgroup check. Same outputs
+// (code, stored f and r sigma, fused level-0 fold) as k_vm_vote.
+__global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
+                                                  PkSrc pk, const uint8_t* __restrict__ sigs, Slab s, uint64_t seed,
+                                                  uint64_t base, int32_t* __restrict__ codes, Slab part0) {
+  __builtin_amdgcn_s_setprio(2);
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
-  const uint32_t slice = threadIdx.x / VM_PAIRCHK_W, lane = threadIdx.x % VM_PAIRCHK_W;
-  uint32_t* slots = lds + VM_NCONST * 12 + slice * VM_PAIRCHK_NSLOTS * 12;
+  const uint32_t slice = threadIdx.x / VM_VOTE_T_W, lane = threadIdx.x % VM_VOTE_T_W;
+  uint32_t* slots = lds + VM_NCONST * 12 + slice * (VM_VOTE_T_NSLOTS * 12 + 4);
+  uint32_t* hdr = slots + VM_VOTE_T_NSLOTS * 12;  // [sig flags, pk flags]
   const uint32_t i = blockIdx.x * VM_SLICES + slice;
-  const bool active = i < n && codes[i] == 0;
+  const bool active = i < n;
   load_consts(cst, cst_g, VM_NCONST);
-  if (active)
-    for (uint32_t k = lane; k < 12; k += VM_PAIRCHK_W) {
+  if (active) {
+    const uint32_t e = pk.idx ? (uint32_t)pk.idx[i] : i;
+    if (lane == 0) {
+      uint32_t x1[12], x0[12], bad, inf, sort, xz;
+      parse_hdr(sigs + (size_t)i * 96, 96, x1, x0, bad, inf, sort, xz);
+      slot_put(slots, VM_VOTE_T_IN[VM_VOTE_T_IN_SIG_X1], x1);
+      slot_put(slots, VM_VOTE_T_IN[VM_VOTE_T_IN_SIG_X0], x0);
+      slot_flag(slots, VM_VOTE_T_IN[VM_VOTE_T_IN_SIG_SORT], sort);
+      hdr[0] = bad | inf << 1 | xz << 2;
+      hdr[1] = pk.flags[e];
+    } else if (lane >= 2 && lane < 6) {
+      Fp u;
+      s.ld(u, S_U + (lane - 2), i);
+      slot_put(slots, VM_VOTE_T_IN[VM_VOTE_T_IN_U00 + (lane - 2)], u.v);
+    } else if (lane >= 6 && lane < 9) {
       Fp v;
-      s.ld(v, S_FB + k, i);
-      slot_put(slots, VM_PAIRCHK_IN[k], v.v);
+      Slab{const_cast<uint32_t*>(pk.planes), pk.cap}.ld(v, lane - 6, e);
+      slot_put(slots, VM_VOTE_T_IN[VM_VOTE_T_IN_PK_X + (lane - 6)], v.v);
     }
+  }
   __syncthreads();
-  vm::run(prog.code, VM_PAIRCHK_NPHASES, VM_PAIRCHK_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0},
-          blockIdx.x == 0 ? prog.trace : nullptr);
-  if (active && lane == 0) codes[i] = slot_flag_get(slots, VM_PAIRCHK_OUT[0]) ? 0 : BLST_VERIFY_FAIL;
+  vm::run(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
+          vm::Out{s.p, s.cap, i}, blockIdx.x == 0 ? prog.trace : nullptr);
+  if (active && lane == 0) {
+    const uint32_t sf = hdr[0], pf = hdr[1];
+    const uint32_t sg_bad = sf & 1, sg_inf = (sf >> 1) & 1, sg_xz = (sf >> 2) & 1;
+    const uint32_t sg_ok = slot_flag_get(slots, VM_VOTE_T_OUT[VM_VOTE_T_OUT_SIG_OK]);
+    const uint32_t sg_grp = slot_flag_get(slots, VM_VOTE_T_OUT[VM_VOTE_T_OUT_SIG_GRP]);
+    const uint32_t h_inf = slot_flag_get(slots, VM_VOTE_T_OUT[VM_VOTE_T_OUT_H_INF]);
+    int32_t c;  // precedence as k_vm_vote (consensus.rs:397-416)
+    if (pf & PKF_PARSE) c = OVH_ERR_PUBKEY;
+    else if (sg_bad) c = BLST_BAD_ENCODING;
+    else if (!sg_inf && !sg_ok) c = BLST_POINT_NOT_ON_CURVE;
+    else if (!sg_inf && (sg_xz || !sg_grp)) c = BLST_POINT_NOT_IN_GROUP;
+    else if (pf & PKF_INF) c = BLST_PK_IS_INFINITY;
+    else if (pf & PKF_GRP) c = BLST_POINT_NOT_IN_GROUP;
+    else if (h_inf || sg_inf) c = BLST_VERIFY_FAIL;
+    else c = 0;
+    codes[i] = c;
+  }
+  __threadfence();
+  __syncthreads();
+  fold_unit(blockIdx.x, n, fold, cst, lds + VM_NCONST * 12, threadIdx.x % VM_FOLD_W,
+            threadIdx.x < VM_FOLD_W && 4 * blockIdx.x < n,
+            Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{s.p + (size_t)S_RS * 12 * s.cap, s.cap}, part0,
+            codes);
+}
+
+// The final program on one unit given as (F planes, S planes) at index u (the other three
+// partials are the identity): prod F * Miller(-G1, S) -> FE == 1.
+__device__ __forceinline__ bool final_one(uint32_t u, const VmDev& prog, const uint32_t* __restrict__ cst_g, Slab inF,
+                                          Slab inS) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  uint32_t* slots = lds + VM_NCONST * 12;
+  const uint32_t lane = threadIdx.x;
+  load_consts(cst, cst_g, VM_NCONST);
+  for (uint32_t k = lane; k < 4 * PART_PLANES; k += 64) {
+    const uint32_t q = k / PART_PLANES, j = k % PART_PLANES;
+    Fp v;
+    if (q == 0) {
+      if (j < 12) inF.ld(v, j, u);
+      else inS.ld(v, j - 12, u);
+    } else if (j == 0 || j == 12 + 2) {
+      fp_one(v);
+    } else {
+      fp_zero(v);
+    }
+    slot_put(slots, VM_FINAL_IN[k], v.v);
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  return slot_flag_get(slots, VM_FINAL_OUT[0]) != 0;
+}
+
+// Bisection, level 1 (only when the combined check failed, *verdict == 0; verdict null: always):
+// grp_ok[g] := the group of votes 16g .. 16g + 15 passes its own combined check.
+#define GROUP_VOTES 16
+__global__ __launch_bounds__(64) void k_vm_group(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
+                                                 Slab inS, const int32_t* __restrict__ verdict,
+                                                 int32_t* __restrict__ grp_ok) {
+  if (verdict && *verdict == 1) return;
+  const uint32_t g = blockIdx.x;
+  if (g >= m) return;
+  const bool ok = final_one(g, prog, cst_g, inF, inS);
+  if (threadIdx.x == 0) grp_ok[g] = ok ? 1 : 0;
+}
+
+// Bisection, vote level: every vote of a failing group whose code is still 0 is checked on its
+// own stored (f_i, r_i sigma_i): e(r pk, H) e(-G1, r sigma) = (e(pk, H) / e(G1, sigma))^r,
+// r != 0 mod the group order, so it is 1 exactly when the vote verifies (the per-call verdict).
+__global__ __launch_bounds__(64) void k_vm_votechk(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g, Slab s,
+                                                   int32_t* __restrict__ codes, const int32_t* __restrict__ verdict,
+                                                   const int32_t* __restrict__ grp_ok) {
+  if (verdict && *verdict == 1) return;
+  const uint32_t i = blockIdx.x;
+  if (i >= n || codes[i] != 0 || grp_ok[i / GROUP_VOTES]) return;
+  const bool ok = final_one(i, prog, cst_g, Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap},
+                            Slab{s.p + (size_t)S_RS * 12 * s.cap, s.cap});
+  if (threadIdx.x == 0) codes[i] = ok ? 0 : BLST_VERIFY_FAIL;
+}
+
+// Validator table (ovh_set_validators): lane per key, 48-byte compressed -> flags + the point
+// (X : Y : Z) Montgomery, (0 : 1 : 0) for infinity or a failed parse.
+__global__ __launch_bounds__(WG) void k_table_build(uint32_t n, const uint8_t* __restrict__ pks, Slab pts,
+                                                    uint32_t* __restrict__ flags) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  G1A a;
+  bool inf;
+  const int e = g1_from_bytes(a, inf, pks + (size_t)i * 48, 48);
+  uint32_t f = 0;
+  Fp X, Y, Z;
+  fp_zero(X);
+  fp_one(Y);
+  fp_zero(Z);
+  if (e != BLST_SUCCESS) {
+    f = PKF_PARSE;
+  } else if (inf) {
+    f = PKF_INF;
+  } else {
+    X = a.x;
+    Y = a.y;
+    fp_one(Z);
+    G1J j;
+    jac_from_aff(j, a);
+    if (!g1_in_subgroup(j)) f = PKF_GRP;
+  }
+  pts.st(X, 0, i);
+  pts.st(Y, 1, i);
+  pts.st(Z, 2, i);
+  flags[i] = f;
+}
+
+// QC batch: lane per QC, apk = sum of the table keys selected by the QC's voter list
+// (sorted-order indices, CSR), homogeneous projective (X Z : Y : Z^3) from Jacobian; flags:
+// PKF_INF when the sum is O.
+__global__ __launch_bounds__(WG) void k_qc_apk(uint32_t nq, const uint32_t* __restrict__ off,
+                                               const uint32_t* __restrict__ ent, Slab table, Slab out,
+                                               uint32_t* __restrict__ flags) {
+  const uint32_t q = blockIdx.x * WG + threadIdx.x;
+  if (q >= nq) return;
+  G1J acc, x;
+  jac_set_inf(acc);
+  for (uint32_t k = off[q]; k < off[q + 1]; ++k) {
+    const uint32_t e = ent[k];
+    table.ld(x.X, 0, e);
+    table.ld(x.Y, 1, e);
+    table.ld(x.Z, 2, e);
+    jac_add(acc, acc, x);
+  }
+  Fp X, Y, Z;
+  uint32_t f = 0;
+  if (jac_is_inf(acc)) {
+    fp_zero(X);
+    fp_one(Y);
+    fp_zero(Z);
+    f = PKF_INF;
+  } else {
+    Fp zz;
+    fp_mul(X, acc.X, acc.Z);
+    Y = acc.Y;
+    fp_sqr(zz, acc.Z);
+    fp_mul(Z, zz, acc.Z);
+  }
+  out.st(X, 0, q);
+  out.st(Y, 1, q);
+  out.st(Z, 2, q);
+  flags[q] = f;
 }
 
 // AoS partials (216 words: F 144, S 72) -> planes
@@ -530,39 +720,72 @@ __global__ __launch_bounds__(WG) void k_sk_to_pk(uint32_t n, const uint8_t* __re
 }
 
 // ------------------------------------------------------------------------ host side
+// Validator table (ovh_set_validators): keys as points in HBM + host lookup structures.
+struct ValidatorTable {
+  uint32_t n = 0, cap = 0;
+  uint32_t* planes = nullptr;   // X, Y, Z planes of `cap` entries
+  uint32_t* flags = nullptr;    // device PKF_* per entry
+  std::vector<uint32_t> hflags;  // host copy
+  std::vector<std::string> keys;
+  std::unordered_map<std::string, uint32_t> index;  // key bytes -> first entry
+  std::vector<uint32_t> sorted;                     // entries by key bytes (overlord authority order)
+};
+
+// Verdict cache of ovh_prefetch: exact (sig, hash, voter) bytes -> per-vote code.
+struct VerdictCache {
+  std::mutex mu;
+  std::unordered_map<std::string, int32_t> map;
+  std::deque<std::string> fifo;
+  size_t cap = 1u << 16;
+  uint64_t hits = 0, misses = 0;
+};
+
 struct ovh_ctx {
   int device = 0;
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
-  // pipelined batches (ovh_verify_batch_device_async): the final check + fallback of batch k run
-  // on fstream while batch k + 1's per-vote stages run on stream; OVH_BATCH_SLOTS slots of batch
-  // state rotate (a slot is reused only after its final-stream work finished).
+  // pipelined batches (ovh_verify_batch_device_async): the final check + bisection of batch k
+  // run on fstream while batch k + 1's per-vote stages run on stream; OVH_BATCH_SLOTS slots of
+  // batch state rotate (a slot is reused only after its final-stream work finished).
   hipStream_t fstream = nullptr;
   hipStream_t hstream = nullptr;  // hash_to_field of the next batch, beside the current vote
   hipEvent_t ev_h[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
+  hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
   uint32_t* state_slot[OVH_BATCH_SLOTS] = {};
-  uint32_t* red_slot[OVH_BATCH_SLOTS] = {};
-  uint32_t* fin = nullptr;       // OVH_BATCH_SLOTS x FIN_STRIDE words: per-slot combine scratch
+  uint32_t* red_slot[OVH_BATCH_SLOTS] = {};  // fold regions R0..R3 (R1: the 16-vote groups)
+  int32_t* grp_ok[OVH_BATCH_SLOTS] = {};
+  uint32_t slot_n[OVH_BATCH_SLOTS] = {};
+  uint32_t* fin = nullptr;  // OVH_BATCH_SLOTS x FIN_STRIDE words: per-slot combine scratch
   uint32_t pipe_k = 0;
   int last_slot = 0;
   XmdTemplates xmd;
-  std::mutex mu;  // Crypto is Send + Sync: serialise device use per context
-  // batch buffers
-  uint32_t cap = 0;
-  uint32_t* state = nullptr;     // S_TOTAL Fp slabs, cap each
-  uint32_t* red = nullptr;       // reduction scratch: 2 x (12 + 6) Fp slabs of cap/8
-  uint32_t red_cap = 0;
-  int32_t* st_pk = nullptr;
-  int32_t* st_sig = nullptr;
-  int32_t* codes = nullptr;      // internal codes for host-pointer API
-  uint8_t* in_buf = nullptr;     // staging for host inputs
+  std::mutex mu;  // Crypto is Send + Sync: every entry point holds it for its whole call
+  uint32_t cap = 0, red_cap = 0;
+  uint8_t* in_buf = nullptr;   // staging for host inputs
   size_t in_cap = 0;
-  uint32_t* partial = nullptr;   // 216 words
-  int32_t* result = nullptr;     // device scalar
+  // single-call scratch (aggregation, sums): separate from the batch slots
+  uint32_t* scr = nullptr;
+  int32_t *scr_pk = nullptr, *scr_sig = nullptr;
+  uint32_t scr_cap = 0;
+  uint32_t* comb = nullptr;  // ovh_combine_partials_device scratch
+  uint32_t comb_cap = 0;
+  uint32_t* part_out = nullptr;  // multi-device: this device's partial (216 words)
+  int32_t* result = nullptr;     // device verdict words
   uint32_t last_n = 0;
+  // RLC coefficients: fresh getrandom seed per batch, or the test seed (OVH_FLAG_TEST_RLC)
+  uint64_t test_seed = 0, test_base = 0;
+  ValidatorTable tab;
+  uint32_t* qc_buf = nullptr;  // QC batch: apk planes + flags
+  uint32_t qc_cap = 0;
+  VerdictCache cache;
+  // multi-device (ovh_create_multi): sub-contexts, one per device; the root owns no streams
+  std::vector<ovh_ctx*> sub;
+  std::atomic<uint32_t> rr{0};
+  uint8_t* gather = nullptr;  // on sub[0]'s device: ndev x 864 B
+  uint32_t* mfin = nullptr;   // on sub[0]'s device: unpack scratch of the gathered partials
   // Fp-VM programs + constant table in device memory
-  VmDev vm_vote{}, vm_fold{}, vm_final{}, vm_pairchk{};
+  VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{};
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
@@ -574,19 +797,26 @@ struct ovh_ctx {
   do {                                             \
     if ((x) != hipSuccess) return OVH_ERR_DEVICE;  \
   } while (0)
+#define CHK(x)                \
+  do {                              \
+    const int e_ = (x);             \
+    if (e_) return e_;              \
+  } while (0)
 
-static const char* const STAGE_NAMES[OVH_NSTAGES] = {"hash_to_field", "vote", "fold", "final", "fallback"};
+static const char* const STAGE_NAMES[OVH_NSTAGES] = {"hash_to_field", "vote", "fold", "final", "bisect"};
 
 // LDS bytes of the VM kernels: constants + slices x slots (+ a 16-byte slice header for vote)
 static constexpr size_t LDS_VOTE = (size_t)VM_NCONST * 48 + VM_SLICES * ((size_t)VM_VOTE_NSLOTS * 48 + 16);
+static constexpr size_t LDS_VOTE_T = (size_t)VM_NCONST * 48 + VM_SLICES * ((size_t)VM_VOTE_T_NSLOTS * 48 + 16);
 static constexpr size_t LDS_FOLD = (size_t)VM_NCONST * 48 + VM_FOLD_UNITS * (size_t)VM_FOLD_NSLOTS * 48;
 static constexpr size_t LDS_FINAL = (size_t)VM_NCONST * 48 + (size_t)VM_FINAL_NSLOTS * 48;
-static constexpr size_t LDS_PAIRCHK = (size_t)VM_NCONST * 48 + VM_SLICES * (size_t)VM_PAIRCHK_NSLOTS * 48;
-static_assert(VM_VOTE_W * VM_SLICES == 64 && VM_FOLD_W * VM_FOLD_UNITS == 64 && VM_PAIRCHK_W * VM_SLICES == 64 &&
+static_assert(VM_VOTE_W * VM_SLICES == 64 && VM_VOTE_T_W * VM_SLICES == 64 && VM_FOLD_W * VM_FOLD_UNITS == 64 &&
                   VM_FINAL_W == 64, "VM slice widths");
 static constexpr size_t LDS_FOLD1 = (size_t)VM_NCONST * 48 + (size_t)VM_FOLD_NSLOTS * 48;
-static_assert(LDS_VOTE <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
-static_assert(VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_NSLOTS * 12 + 4), "fused fold reuses the vote slots");
+static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
+static_assert(VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_NSLOTS * 12 + 4) &&
+                  VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_T_NSLOTS * 12 + 4),
+              "fused fold reuses the vote slots");
 
 static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphases, uint32_t W, const uint16_t* in,
                      uint32_t nin, const uint16_t* out, uint32_t nout) {
@@ -620,26 +850,25 @@ static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphase
 static int vm_init(ovh_ctx* c) {
   HIPCHK(hipMalloc(&c->vm_consts, sizeof(VM_CONST_WORDS)));
   HIPCHK(hipMemcpy(c->vm_consts, VM_CONST_WORDS, sizeof(VM_CONST_WORDS), hipMemcpyHostToDevice));
-  if (vm_upload(c, c->vm_vote, VM_VOTE_CODE, VM_VOTE_NPHASES, VM_VOTE_W, VM_VOTE_IN, VM_VOTE_NIN, VM_VOTE_OUT,
-                VM_VOTE_NOUT) ||
-      vm_upload(c, c->vm_fold, VM_FOLD_CODE, VM_FOLD_NPHASES, VM_FOLD_W, VM_FOLD_IN, VM_FOLD_NIN, VM_FOLD_OUT,
-                VM_FOLD_NOUT) ||
-      vm_upload(c, c->vm_final, VM_FINAL_CODE, VM_FINAL_NPHASES, VM_FINAL_W, VM_FINAL_IN, VM_FINAL_NIN,
-                VM_FINAL_OUT, VM_FINAL_NOUT) ||
-      vm_upload(c, c->vm_pairchk, VM_PAIRCHK_CODE, VM_PAIRCHK_NPHASES, VM_PAIRCHK_W, VM_PAIRCHK_IN,
-                VM_PAIRCHK_NIN, VM_PAIRCHK_OUT, VM_PAIRCHK_NOUT))
-    return OVH_ERR_DEVICE;
+  CHK(vm_upload(c, c->vm_vote, VM_VOTE_CODE, VM_VOTE_NPHASES, VM_VOTE_W, VM_VOTE_IN, VM_VOTE_NIN, VM_VOTE_OUT,
+                VM_VOTE_NOUT));
+  CHK(vm_upload(c, c->vm_vote_t, VM_VOTE_T_CODE, VM_VOTE_T_NPHASES, VM_VOTE_T_W, VM_VOTE_T_IN, VM_VOTE_T_NIN,
+                VM_VOTE_T_OUT, VM_VOTE_T_NOUT));
+  CHK(vm_upload(c, c->vm_fold, VM_FOLD_CODE, VM_FOLD_NPHASES, VM_FOLD_W, VM_FOLD_IN, VM_FOLD_NIN, VM_FOLD_OUT,
+                VM_FOLD_NOUT));
+  CHK(vm_upload(c, c->vm_final, VM_FINAL_CODE, VM_FINAL_NPHASES, VM_FINAL_W, VM_FINAL_IN, VM_FINAL_NIN, VM_FINAL_OUT,
+                VM_FINAL_NOUT));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE));
+  HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote_t, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE_T));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold<VM_FOLD_UNITS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)LDS_FOLD));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FOLD1));
-  HIPCHK(hipFuncSetAttribute((const void*)k_vm_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FINAL));
-  HIPCHK(hipFuncSetAttribute((const void*)k_vm_pairchk, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)LDS_PAIRCHK));
+  for (const void* k : {(const void*)k_vm_final, (const void*)k_vm_group, (const void*)k_vm_votechk})
+    HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FINAL));
   return 0;
 }
 
-// Stage bracket: events on the context's stream around the stage's kernels.
+// Stage bracket: events on a stream around the stage's kernels.
 struct StageScope {
   ovh_ctx* c;
   int k;
@@ -655,57 +884,69 @@ struct StageScope {
   }
 };
 
-
 static const uint8_t DEFAULT_DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_";
 
 static uint32_t nblk(size_t n) { return (uint32_t)((n + WG - 1) / WG); }
 
+// ---- buffers
+static Slab region_F(ovh_ctx* c, int slot, int r) {
+  return Slab{c->red_slot[slot] + (size_t)r * PART_PLANES * 12 * c->red_cap, c->red_cap};
+}
+static Slab region_S(ovh_ctx* c, int slot, int r) {
+  return Slab{c->red_slot[slot] + (size_t)r * PART_PLANES * 12 * c->red_cap + (size_t)12 * 12 * c->red_cap,
+              c->red_cap};
+}
+
+static int sync_all(ovh_ctx* c) {
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipStreamSynchronize(c->fstream));
+  HIPCHK(hipStreamSynchronize(c->hstream));
+  return 0;
+}
+
+// Batch state for n votes: per slot S_TOTAL planes, fold regions R0..R3 (cap/4 partials each)
+// and the group verdicts. A reallocation waits for all work and forgets the last batch.
 static int ensure_cap(ovh_ctx* c, size_t n) {
   if (n > (1u << 24)) return OVH_ERR_ARG;
-  if (n <= c->cap && c->state) return 0;
+  if (n <= c->cap && c->state_slot[0]) return 0;
   uint32_t cap = 256;
   while (cap < n) cap <<= 1;
-  HIPCHK(hipStreamSynchronize(c->stream));
-  if (c->fstream) HIPCHK(hipStreamSynchronize(c->fstream));
-  if (c->hstream) HIPCHK(hipStreamSynchronize(c->hstream));
+  CHK(sync_all(c));
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
-    if (c->state_slot[k]) (void)hipFree(c->state_slot[k]);
-    if (c->red_slot[k]) (void)hipFree(c->red_slot[k]);
+    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k]})
+      if (p) (void)hipFree(p);
     c->state_slot[k] = c->red_slot[k] = nullptr;
+    c->grp_ok[k] = nullptr;
+    c->slot_n[k] = 0;
   }
-  if (c->st_pk) (void)hipFree(c->st_pk);
-  if (c->st_sig) (void)hipFree(c->st_sig);
-  if (c->codes) (void)hipFree(c->codes);
-  c->state = nullptr;
-  c->red = nullptr;
+  c->last_n = 0;
+  c->cap = 0;
   c->red_cap = cap / 4 > 64 ? cap / 4 : 64;
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
     HIPCHK(hipMalloc(&c->state_slot[k], (size_t)S_TOTAL * 12 * cap * 4));
-    HIPCHK(hipMalloc(&c->red_slot[k], (size_t)2 * PART_PLANES * 12 * c->red_cap * 4));
+    HIPCHK(hipMalloc(&c->red_slot[k], (size_t)4 * PART_PLANES * 12 * c->red_cap * 4));
+    HIPCHK(hipMalloc(&c->grp_ok[k], ((size_t)cap / GROUP_VOTES + 1) * 4));
   }
-  c->state = c->state_slot[0];
-  c->red = c->red_slot[0];
-  HIPCHK(hipMalloc(&c->st_pk, (size_t)cap * 4));
-  HIPCHK(hipMalloc(&c->st_sig, (size_t)cap * 4));
-  HIPCHK(hipMalloc(&c->codes, (size_t)cap * 4));
   c->cap = cap;
   return 0;
 }
 
-// Wait for pipelined batch work on the final stream (APIs that reuse the batch state as
-// scratch call this first).
-static int drain(ovh_ctx* c) {
-  if (c->fstream) HIPCHK(hipStreamSynchronize(c->fstream));
-  return 0;
-}
-
-// Batch state slot k for the next batch on the main stream: the stream first waits until the
-// final stream has finished with the slot's previous batch (its fallback reads that state).
-static int take_slot(ovh_ctx* c, int k) {
-  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_back[k], 0));
-  c->state = c->state_slot[k];
-  c->red = c->red_slot[k];
-  c->last_slot = k;
+// Single-call scratch (aggregation / key sums): 9 planes + two code arrays of n entries.
+static int ensure_scr(ovh_ctx* c, size_t n) {
+  if (n > (1u << 24)) return OVH_ERR_ARG;
+  if (n <= c->scr_cap && c->scr) return 0;
+  uint32_t cap = 256;
+  while (cap < n) cap <<= 1;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (void* p : {(void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig})
+    if (p) (void)hipFree(p);
+  c->scr = nullptr;
+  c->scr_pk = c->scr_sig = nullptr;
+  c->scr_cap = 0;
+  HIPCHK(hipMalloc(&c->scr, (size_t)9 * 12 * cap * 4));
+  HIPCHK(hipMalloc(&c->scr_pk, (size_t)cap * 4));
+  HIPCHK(hipMalloc(&c->scr_sig, (size_t)cap * 4));
+  c->scr_cap = cap;
   return 0;
 }
 
@@ -713,14 +954,368 @@ static int ensure_in(ovh_ctx* c, size_t bytes) {
   if (bytes <= c->in_cap && c->in_buf) return 0;
   size_t cap = 4096;
   while (cap < bytes) cap <<= 1;
+  HIPCHK(hipStreamSynchronize(c->stream));
   if (c->in_buf) (void)hipFree(c->in_buf);
   c->in_buf = nullptr;
+  c->in_cap = 0;
   HIPCHK(hipMalloc(&c->in_buf, cap));
   c->in_cap = cap;
   return 0;
 }
 
+// Batch state slot k for the next batch on the main stream: the stream first waits until the
+// final stream has finished with the slot's previous batch (its bisection reads that state).
+static int take_slot(ovh_ctx* c, int* slot) {
+  const int k = (int)(c->pipe_k++ % OVH_BATCH_SLOTS);
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_back[k], 0));
+  c->last_slot = k;
+  *slot = k;
+  return 0;
+}
+
+// RLC coefficients of the next batch: SplitMix64(seed, base + i) with a fresh secret seed from
+// the OS (the coefficients must be unknown to whoever produced the signatures).
+static int draw_seed(ovh_ctx* c, uint64_t* seed, uint64_t* base) {
+  if (c->flags & OVH_FLAG_TEST_RLC) {
+    *seed = c->test_seed;
+    *base = c->test_base;
+    return 0;
+  }
+  uint8_t b[8];
+  size_t got = 0;
+  while (got < sizeof b) {
+    const ssize_t r = getrandom(b + got, sizeof b - got, 0);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return OVH_ERR_RNG;
+    }
+    got += (size_t)r;
+  }
+  memcpy(seed, b, 8);
+  *base = 0;
+  return 0;
+}
+
+// Key source of a batch: compressed bytes (vote program) or points (vote_t program).
+struct KeySrc {
+  const uint8_t* bytes;  // n x 48, or null
+  PkSrc pts;
+};
+
+// Per-vote stages of a batch in `slot`: hash_to_field, the vote kernel with fold level 0 fused
+// (-> R0), fold level 1 (-> R1: one partial per 16-vote group, kept for the bisection).
+static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
+                       int32_t* d_codes, bool pipelined) {
+  Slab s{c->state_slot[slot], c->cap};
+  hipStream_t st = c->stream;
+  c->ev_mask = 0;
+  uint64_t seed, base;
+  CHK(draw_seed(c, &seed, &base));
+  const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
+  if (pipelined) {
+    // hash_to_field on its own stream, as soon as the slot's previous batch has finished its
+    // per-vote stages (the only reader of the S_U planes), so it runs beside the current vote
+    // kernel; the vote waits for it
+    HIPCHK(hipStreamWaitEvent(c->hstream, c->ev_front[slot], 0));
+    {
+      StageScope p(c, ST_H2F, c->hstream);
+      k_h2f<<<nblk(n), WG, 0, c->hstream>>>(n, d_hashes, c->xmd, s);
+    }
+    HIPCHK(hipEventRecord(c->ev_h[slot], c->hstream));
+    HIPCHK(hipStreamWaitEvent(st, c->ev_h[slot], 0));
+  } else {
+    StageScope p(c, ST_H2F);
+    k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s);
+  }
+  {
+    StageScope p(c, ST_VOTE);
+    if (key.bytes)
+      k_vm_vote<<<nwg, 64, LDS_VOTE, st>>>(n, c->vm_vote, c->vm_fold, c->vm_consts, key.bytes, d_sigs, s, seed, base,
+                                           d_codes, region_F(c, slot, 0));
+    else
+      k_vm_vote_t<<<nwg, 64, LDS_VOTE_T, st>>>(n, c->vm_vote_t, c->vm_fold, c->vm_consts, key.pts, d_sigs, s, seed,
+                                               base, d_codes, region_F(c, slot, 0));
+  }
+  {
+    StageScope p(c, ST_FOLD);
+    const uint32_t m1 = (nwg + 3) / 4;
+    k_vm_fold<VM_FOLD_UNITS><<<(m1 + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(
+        nwg, c->vm_fold, c->vm_consts, region_F(c, slot, 0), region_S(c, slot, 0), region_F(c, slot, 1), nullptr);
+  }
+  HIPCHK(hipGetLastError());
+  c->slot_n[slot] = n;
+  c->last_n = n;
+  return 0;
+}
+
+static uint32_t groups_of(uint32_t n) { return (n + GROUP_VOTES - 1) / GROUP_VOTES; }
+
+// Fold levels from region *reg (m partials) down to <= until, on stream st, alternating regions
+// R2 / R3 (R1 stays intact for the bisection). slices = 4 (main stream) or 1 (the final
+// stream, beside the next batch's vote workgroups).
+static int fold_down(ovh_ctx* c, int slot, hipStream_t st, int slices, int* reg, uint32_t* m, uint32_t until) {
+  StageScope p(c, ST_FOLD, st);
+  while (*m > until) {
+    const uint32_t mo = (*m + 3) / 4;
+    const int ro = *reg == 2 ? 3 : 2;
+    if (slices == 1)
+      k_vm_fold<1><<<mo, 64, LDS_FOLD1, st>>>(*m, c->vm_fold, c->vm_consts, region_F(c, slot, *reg),
+                                              region_S(c, slot, *reg), region_F(c, slot, ro), nullptr);
+    else
+      k_vm_fold<VM_FOLD_UNITS><<<(mo + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(
+          *m, c->vm_fold, c->vm_consts, region_F(c, slot, *reg), region_S(c, slot, *reg), region_F(c, slot, ro),
+          nullptr);
+    *reg = ro;
+    *m = mo;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
+}
+
+// Verdict words in c->result: [0] single calls, then per slot the batch verdicts, the combine
+// verdicts, then the synchronous combine's and the multi-device combine's.
+enum { RES_BATCH = 4, RES_COMBINE = RES_BATCH + OVH_BATCH_SLOTS, RES_SYNC = RES_COMBINE + OVH_BATCH_SLOTS, RES_MULTI };
+static_assert(RES_MULTI < 16, "verdict words fit c->result");
+
+// Final check on <= 4 partials given as planes: k_vm_final on stream `st`, verdict to *d_res.
+static void enqueue_final(ovh_ctx* c, hipStream_t st, Slab F, Slab S, uint32_t m, int32_t* d_res) {
+  StageScope p(c, ST_FINAL, st);
+  k_vm_final<<<1, 64, LDS_FINAL, st>>>(m, c->vm_final, c->vm_consts, F, S, d_res);
+}
+
+// Bisection of the batch in `slot` on stream `st`, skipped on the device when *d_verdict == 1
+// (d_verdict null: always runs): the 16-vote groups' own checks (R1 partials), then per-vote
+// checks of the votes in failing groups.
+static void enqueue_bisect(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, int32_t* d_codes,
+                           const int32_t* d_verdict) {
+  StageScope p(c, ST_FALLBACK, st);
+  const uint32_t g = groups_of(n);
+  k_vm_group<<<g, 64, LDS_FINAL, st>>>(g, c->vm_final, c->vm_consts, region_F(c, slot, 1), region_S(c, slot, 1),
+                                       d_verdict, c->grp_ok[slot]);
+  k_vm_votechk<<<n, 64, LDS_FINAL, st>>>(n, c->vm_final, c->vm_consts, Slab{c->state_slot[slot], c->cap}, d_codes,
+                                         d_verdict, c->grp_ok[slot]);
+}
+
+// One batch, pipelined: per-vote stages + wide fold levels on the main stream; the narrow fold
+// levels, the combined check and the gated bisection on the final stream. Caller holds c->mu.
+static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
+                               int32_t* d_codes) {
+  CHK(ensure_cap(c, n));
+  int slot;
+  CHK(take_slot(c, &slot));
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, true));
+  uint32_t m = groups_of((uint32_t)n);
+  int reg = 1;
+  CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 64));
+  HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
+  HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_front[slot], 0));
+  CHK(fold_down(c, slot, c->fstream, 1, &reg, &m, 4));
+  int32_t* verdict = c->result + RES_BATCH + slot;
+  enqueue_final(c, c->fstream, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict);
+  enqueue_bisect(c, c->fstream, slot, (uint32_t)n, d_codes, verdict);
+  HIPCHK(hipEventRecord(c->ev_back[slot], c->fstream));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// Host inputs -> staging buffer (sigs, hashes, pks, codes) on the main stream.
+static int stage_batch(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                       uint8_t** d) {
+  CHK(ensure_in(c, n * (96 + 32 + 48 + 4 + 4) + 64));
+  *d = c->in_buf;
+  HIPCHK(hipMemcpyAsync(*d, sigs, n * 96, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(*d + n * 96, hashes, n * 32, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(*d + n * 128, pks, n * 48, hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
+// The table entry of each voter (all found: true, idx filled) -- the vote_t path.
+static bool table_lookup(ovh_ctx* c, size_t n, const uint8_t* pks, std::vector<int32_t>& idx) {
+  if (!c->tab.n) return false;
+  idx.resize(n);
+  std::string k(48, '\0');
+  for (size_t i = 0; i < n; ++i) {
+    memcpy(&k[0], pks + 48 * i, 48);
+    auto it = c->tab.index.find(k);
+    if (it == c->tab.index.end()) return false;
+    idx[i] = (int32_t)it->second;
+  }
+  return true;
+}
+
+// ovh_verify_batch on one device (caller holds c->mu): codes (host) of n votes.
+static int verify_host_locked(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                              int32_t* codes) {
+  HIPCHK(hipSetDevice(c->device));
+  uint8_t* d;
+  CHK(stage_batch(c, n, sigs, hashes, pks, &d));
+  int32_t* dc = (int32_t*)(d + n * 176);
+  std::vector<int32_t> idx;
+  KeySrc key{d + n * 128, PkSrc{}};
+  if (table_lookup(c, n, pks, idx)) {
+    int32_t* di = dc + n;
+    HIPCHK(hipMemcpyAsync(di, idx.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+    key = KeySrc{nullptr, PkSrc{c->tab.planes, c->tab.cap, c->tab.flags, di}};
+  }
+  CHK(verify_async_locked(c, n, d, d + n * 96, key, dc));
+  CHK(sync_all(c));
+  HIPCHK(hipMemcpyAsync(codes, dc, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// Per-shard partial of `slot` (folded to one) -> AoS at `out` (device), on the main stream.
+static int shard_partial(ovh_ctx* c, int slot, uint32_t n, uint32_t* out, hipStream_t wait_on) {
+  uint32_t m = groups_of(n);
+  int reg = 1;
+  CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 1));
+  if (wait_on) {  // the caller's earlier work on its stream (e.g. a gather reading `out`) first
+    HIPCHK(hipEventRecord(c->ev_x[0], wait_on));
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_x[0], 0));
+  }
+  k_pack_partial2<<<1, 64, 0, c->stream>>>(region_F(c, slot, reg), region_S(c, slot, reg), out);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// ---- multi-device (ovh_create_multi)
+static void shard_range(size_t n, size_t nd, size_t d, size_t* lo, size_t* cnt) {
+  const size_t base = n / nd, extra = n % nd;
+  *lo = d * base + (d < extra ? d : extra);
+  *cnt = base + (d < extra ? 1 : 0);
+}
+
+static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                             int32_t* codes) {
+  const size_t nd = root->sub.size();
+  std::vector<std::unique_lock<std::mutex>> locks;  // root (gather scratch), then every device
+  locks.emplace_back(root->mu);
+  for (ovh_ctx* s : root->sub) locks.emplace_back(s->mu);
+  ovh_ctx* s0 = root->sub[0];
+  std::vector<int> slot(nd, 0);
+  std::vector<int32_t*> dcodes(nd, nullptr);
+  size_t k = 0;
+  for (size_t d = 0; d < nd; ++d) {
+    ovh_ctx* s = root->sub[d];
+    size_t lo, cnt;
+    shard_range(n, nd, d, &lo, &cnt);
+    if (!cnt) continue;
+    HIPCHK(hipSetDevice(s->device));
+    uint8_t* in;
+    CHK(stage_batch(s, cnt, sigs + lo * 96, hashes + lo * 32, pks + lo * 48, &in));
+    dcodes[d] = (int32_t*)(in + cnt * 176);
+    std::vector<int32_t> idx;
+    KeySrc key{in + cnt * 128, PkSrc{}};
+    if (table_lookup(s, cnt, pks + lo * 48, idx)) {
+      int32_t* di = dcodes[d] + cnt;
+      HIPCHK(hipMemcpyAsync(di, idx.data(), cnt * 4, hipMemcpyHostToDevice, s->stream));
+      key = KeySrc{nullptr, PkSrc{s->tab.planes, s->tab.cap, s->tab.flags, di}};
+    }
+    CHK(ensure_cap(s, cnt));
+    CHK(take_slot(s, &slot[d]));
+    s->test_base = root->test_base + lo;  // OVH_FLAG_TEST_RLC only: one global index per vote
+    CHK(batch_front(s, slot[d], (uint32_t)cnt, in, in + cnt * 96, key, dcodes[d], false));
+    CHK(shard_partial(s, slot[d], (uint32_t)cnt, s->part_out, nullptr));
+    // partial -> devices[0] (peer copy over xGMI), ordered on this device's stream
+    HIPCHK(hipMemcpyPeerAsync(root->gather + k * OVH_PARTIAL_BYTES, s0->device, s->part_out, s->device,
+                              OVH_PARTIAL_BYTES, s->stream));
+    HIPCHK(hipEventRecord(s->ev_x[1], s->stream));
+    ++k;
+  }
+  if (!k) return 0;
+  HIPCHK(hipSetDevice(s0->device));
+  for (size_t d = 0; d < nd; ++d)
+    if (dcodes[d]) HIPCHK(hipStreamWaitEvent(s0->fstream, root->sub[d]->ev_x[1], 0));
+  Slab uF{root->mfin, 16}, uS{root->mfin + (size_t)12 * 12 * 16, 16};
+  Slab F = uF, S = uS;
+  uint32_t m = (uint32_t)k;
+  k_unpack_partials<<<(uint32_t)((k * PART_PLANES + 63) / 64), 64, 0, s0->fstream>>>((uint32_t)k,
+                                                                                   (const uint32_t*)root->gather, uF, uS);
+  if (k > 4) {
+    uint32_t* o = root->mfin + (size_t)PART_PLANES * 12 * 16;
+    F = Slab{o, 4};
+    S = Slab{o + (size_t)12 * 12 * 4, 4};
+    k_vm_fold<VM_FOLD_UNITS><<<1, 64, LDS_FOLD, s0->fstream>>>((uint32_t)k, s0->vm_fold, s0->vm_consts, uF, uS, F,
+                                                             nullptr);
+    m = (uint32_t)((k + 3) / 4);
+  }
+  enqueue_final(s0, s0->fstream, F, S, m, s0->result + RES_MULTI);
+  HIPCHK(hipGetLastError());
+  int32_t verdict = 0;
+  HIPCHK(hipMemcpyAsync(&verdict, s0->result + RES_MULTI, 4, hipMemcpyDeviceToHost, s0->fstream));
+  HIPCHK(hipStreamSynchronize(s0->fstream));
+  for (size_t d = 0; d < nd; ++d) {
+    if (!dcodes[d]) continue;
+    ovh_ctx* s = root->sub[d];
+    size_t lo, cnt;
+    shard_range(n, nd, d, &lo, &cnt);
+    HIPCHK(hipSetDevice(s->device));
+    if (!verdict) enqueue_bisect(s, s->stream, slot[d], (uint32_t)cnt, dcodes[d], nullptr);
+    HIPCHK(hipMemcpyAsync(codes + lo, dcodes[d], 4 * cnt, hipMemcpyDeviceToHost, s->stream));
+  }
+  for (size_t d = 0; d < nd; ++d)
+    if (dcodes[d]) {
+      HIPCHK(hipSetDevice(root->sub[d]->device));
+      HIPCHK(hipStreamSynchronize(root->sub[d]->stream));
+    }
+  return 0;
+}
+
+static ovh_ctx* pick_sub(ovh_ctx* c) {
+  if (c->sub.empty()) return c;
+  return c->sub[c->rr.fetch_add(1) % c->sub.size()];
+}
+
+// ---- verdict cache
+static std::string cache_key(const uint8_t* sig, const uint8_t* hash, const uint8_t* pk) {
+  std::string k(176, '\0');
+  memcpy(&k[0], sig, 96);
+  memcpy(&k[96], hash, 32);
+  memcpy(&k[128], pk, 48);
+  return k;
+}
+
+static void cache_put(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                      const int32_t* codes) {
+  std::lock_guard<std::mutex> g(c->cache.mu);
+  if (!c->cache.cap) return;
+  for (size_t i = 0; i < n; ++i) {
+    std::string k = cache_key(sigs + 96 * i, hashes + 32 * i, pks + 48 * i);
+    auto it = c->cache.map.find(k);
+    if (it != c->cache.map.end()) {
+      it->second = codes[i];
+      continue;
+    }
+    while (c->cache.map.size() >= c->cache.cap && !c->cache.fifo.empty()) {
+      c->cache.map.erase(c->cache.fifo.front());
+      c->cache.fifo.pop_front();
+    }
+    c->cache.map.emplace(k, codes[i]);
+    c->cache.fifo.push_back(std::move(k));
+  }
+}
+
+static bool cache_get(ovh_ctx* c, const uint8_t* sig, const uint8_t* hash, const uint8_t* pk, int32_t* code) {
+  std::lock_guard<std::mutex> g(c->cache.mu);
+  if (!c->cache.cap) return false;
+  auto it = c->cache.map.find(cache_key(sig, hash, pk));
+  if (it == c->cache.map.end()) {
+    ++c->cache.misses;
+    return false;
+  }
+  ++c->cache.hits;
+  *code = it->second;
+  return true;
+}
+
+// ---- key parse
+static int sk_parse(const ovh_ctx* c, const uint8_t* key, size_t len, uint8_t out[32]) {
+  const bool ok = (c->flags & OVH_FLAG_SK_RAW) ? keygen::sk_raw(out, key, len) : keygen::key_gen(out, key, len);
+  return ok ? 0 : BLST_BAD_ENCODING;
+}
+
 extern "C" {
+
+static void destroy_one(ovh_ctx* c);
 
 ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t flags) {
   if (hipSetDevice(device) != hipSuccess) return nullptr;
@@ -732,88 +1327,114 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
     dst = DEFAULT_DST;
     dst_len = 43;
   }
-  if (!xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) ||
-      hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&c->partial, 216 * 4) != hipSuccess || hipMalloc(&c->result, 64) != hipSuccess) {
-    delete c;
+  int lo = 0, hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
+  bool ok = xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) &&
+            hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) == hipSuccess &&
+            hipMalloc(&c->part_out, 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
+            hipMemset(c->result, 0, 64) == hipSuccess &&
+            hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
+  for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k)
+    ok = hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&c->ev_h[k], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&c->ev_back[k], hipEventDisableTiming) == hipSuccess;
+  for (int k = 0; ok && k < 4; ++k) ok = hipEventCreateWithFlags(&c->ev_x[k], hipEventDisableTiming) == hipSuccess;
+  if (ok && (flags & OVH_FLAG_PROFILE))
+    for (int k = 0; ok && k < OVH_NSTAGES; ++k)
+      ok = hipEventCreate(&c->ev0[k]) == hipSuccess && hipEventCreate(&c->ev1[k]) == hipSuccess;
+  if (!ok) {
+    destroy_one(c);
     return nullptr;
   }
-  if (vm_init(c)) {
-    ovh_destroy(c);
-    return nullptr;
-  }
-  {
-    int lo = 0, hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
-    if (hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) != hipSuccess) {
-      ovh_destroy(c);
-      return nullptr;
-    }
-    for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
-      if (hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&c->ev_h[k], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&c->ev_back[k], hipEventDisableTiming) != hipSuccess) {
-        ovh_destroy(c);
-        return nullptr;
-      }
-  }
-  if (flags & OVH_FLAG_PROFILE)
-    for (int k = 0; k < OVH_NSTAGES; ++k)
-      if (hipEventCreate(&c->ev0[k]) != hipSuccess || hipEventCreate(&c->ev1[k]) != hipSuccess) {
-        ovh_destroy(c);
-        return nullptr;
-      }
   return c;
 }
 
-void ovh_destroy(ovh_ctx* c) {
-  if (!c) return;
-  (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->fstream) (void)hipStreamSynchronize(c->fstream);
-  if (c->hstream) (void)hipStreamSynchronize(c->hstream);
-  for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
-    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k]})
-      if (p) (void)hipFree(p);
-  for (void* p : {(void*)c->st_pk, (void*)c->st_sig, (void*)c->codes, (void*)c->in_buf, (void*)c->partial,
-                  (void*)c->result, (void*)c->vm_consts, (void*)c->fin})
-    if (p) (void)hipFree(p);
-  if (c->fstream) (void)hipStreamDestroy(c->fstream);
-  if (c->hstream) (void)hipStreamDestroy(c->hstream);
-  for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
-    if (c->ev_front[k]) (void)hipEventDestroy(c->ev_front[k]);
-    if (c->ev_h[k]) (void)hipEventDestroy(c->ev_h[k]);
-    if (c->ev_back[k]) (void)hipEventDestroy(c->ev_back[k]);
+ovh_ctx* ovh_create_multi(const int* devices, int ndev, const uint8_t* dst, size_t dst_len, uint32_t flags) {
+  if (!devices || ndev < 1 || ndev > 16) return nullptr;
+  ovh_ctx* root = new (std::nothrow) ovh_ctx();
+  if (!root) return nullptr;
+  root->device = devices[0];
+  root->flags = flags;
+  for (int d = 0; d < ndev; ++d) {
+    ovh_ctx* s = ovh_create(devices[d], dst, dst_len, flags);
+    if (!s) {
+      ovh_destroy(root);
+      return nullptr;
+    }
+    root->sub.push_back(s);
   }
+  for (int d = 1; d < ndev; ++d)
+    if (devices[d] != devices[0]) {  // peer access for the partial copies (xGMI); best effort
+      (void)hipSetDevice(devices[0]);
+      (void)hipDeviceEnablePeerAccess(devices[d], 0);
+      (void)hipSetDevice(devices[d]);
+      (void)hipDeviceEnablePeerAccess(devices[0], 0);
+    }
+  (void)hipGetLastError();
+  if (hipSetDevice(devices[0]) != hipSuccess || hipMalloc(&root->gather, (size_t)16 * OVH_PARTIAL_BYTES) != hipSuccess ||
+      hipMalloc(&root->mfin, FIN_STRIDE * 4) != hipSuccess) {
+    ovh_destroy(root);
+    return nullptr;
+  }
+  return root;
+}
+
+static void destroy_one(ovh_ctx* c) {
+  (void)hipSetDevice(c->device);
+  for (hipStream_t s : {c->stream, c->fstream, c->hstream})
+    if (s) (void)hipStreamSynchronize(s);
+  for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
+    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k]})
+      if (p) (void)hipFree(p);
+  for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vm_consts,
+                  (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
+                  (void*)c->tab.planes, (void*)c->tab.flags, (void*)c->qc_buf, (void*)c->gather, (void*)c->mfin})
+    if (p) (void)hipFree(p);
   for (void* p : c->vm_bufs) (void)hipFree(p);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
+    for (hipEvent_t e : {c->ev_front[k], c->ev_h[k], c->ev_back[k]})
+      if (e) (void)hipEventDestroy(e);
+  for (int k = 0; k < 4; ++k)
+    if (c->ev_x[k]) (void)hipEventDestroy(c->ev_x[k]);
   for (int k = 0; k < OVH_NSTAGES; ++k) {
     if (c->ev0[k]) (void)hipEventDestroy(c->ev0[k]);
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
   }
+  for (hipStream_t s : {c->stream, c->fstream, c->hstream})
+    if (s) (void)hipStreamDestroy(s);
   delete c;
 }
 
+void ovh_destroy(ovh_ctx* c) {
+  if (!c) return;
+  for (ovh_ctx* s : c->sub) destroy_one(s);
+  c->sub.clear();
+  destroy_one(c);
+}
+
+int ovh_device_count(ovh_ctx* c) { return !c ? 0 : c->sub.empty() ? 1 : (int)c->sub.size(); }
+
 int ovh_vm_trace(ovh_ctx* c, int prog, uint64_t* stamps, size_t max) {
   if (!c || prog < 0 || prog > 3 || (max && !stamps)) return -OVH_ERR_ARG;
+  if (!c->sub.empty()) c = c->sub[0];
   if (!(c->flags & OVH_FLAG_VM_TRACE)) return 0;
   std::lock_guard<std::mutex> g(c->mu);
   if (hipSetDevice(c->device) != hipSuccess) return -OVH_ERR_DEVICE;
-  const VmDev* d = prog == 0 ? &c->vm_vote : prog == 1 ? &c->vm_fold : prog == 2 ? &c->vm_final : &c->vm_pairchk;
+  const VmDev* d = prog == 0 ? &c->vm_vote : prog == 1 ? &c->vm_fold : prog == 2 ? &c->vm_final : &c->vm_vote_t;
   const size_t n = (size_t)d->nphases + 1, k = max < n ? max : n;
-  if (hipStreamSynchronize(c->stream) != hipSuccess ||
-      (k && hipMemcpy(stamps, d->trace, k * 8, hipMemcpyDeviceToHost) != hipSuccess))
+  if (sync_all(c) || (k && hipMemcpy(stamps, d->trace, k * 8, hipMemcpyDeviceToHost) != hipSuccess))
     return -OVH_ERR_DEVICE;
   return (int)n;
 }
 
 int ovh_stage_times(ovh_ctx* c, float* ms, size_t max) {
   if (!c || (!ms && max)) return -OVH_ERR_ARG;
+  if (!c->sub.empty()) c = c->sub[0];
   if (!(c->flags & OVH_FLAG_PROFILE)) return 0;
   std::lock_guard<std::mutex> g(c->mu);
-  if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) return -OVH_ERR_DEVICE;
+  if (hipSetDevice(c->device) != hipSuccess || sync_all(c)) return -OVH_ERR_DEVICE;
   const size_t n = max < OVH_NSTAGES ? max : OVH_NSTAGES;
   for (size_t k = 0; k < n; ++k) {
     ms[k] = 0.f;
@@ -825,7 +1446,11 @@ int ovh_stage_times(ovh_ctx* c, float* ms, size_t max) {
 
 const char* ovh_stage_name(int k) { return (k >= 0 && k < OVH_NSTAGES) ? STAGE_NAMES[k] : nullptr; }
 
-void* ovh_stream(ovh_ctx* c) { return c ? (void*)c->stream : nullptr; }
+void* ovh_stream(ovh_ctx* c) {
+  if (!c) return nullptr;
+  if (!c->sub.empty()) c = c->sub[0];
+  return (void*)c->stream;
+}
 
 int ovh_sm3(const uint8_t* msg, size_t len, uint8_t out[32]) {
   if ((!msg && len) || !out) return OVH_ERR_ARG;
@@ -833,25 +1458,20 @@ int ovh_sm3(const uint8_t* msg, size_t len, uint8_t out[32]) {
   return 0;
 }
 
-// 0 < sk < r, 32 bytes big-endian (blst SecretKey::from_bytes)
-static bool sk_valid(const uint8_t* sk, size_t len) {
-  static const uint8_t R_BE[32] = {0x73, 0xed, 0xa7, 0x53, 0x29, 0x9d, 0x7d, 0x48, 0x33, 0x39, 0xd8,
-                                   0x08, 0x09, 0xa1, 0xd8, 0x05, 0x53, 0xbd, 0xa4, 0x02, 0xff, 0xfe,
-                                   0x5b, 0xfe, 0xff, 0xff, 0xff, 0xff, 0x00, 0x00, 0x00, 0x01};
-  if (!sk || len != 32) return false;
-  bool nz = false;
-  for (int i = 0; i < 32; ++i) nz |= sk[i] != 0;
-  if (!nz) return false;
-  return memcmp(sk, R_BE, 32) < 0;
+int ovh_sk_parse(ovh_ctx* c, const uint8_t* key, size_t key_len, uint8_t out_scalar[32]) {
+  if (!c || !out_scalar) return OVH_ERR_ARG;
+  return sk_parse(c, key, key_len, out_scalar);
 }
 
-int ovh_sign(ovh_ctx* c, const uint8_t* sk, size_t sk_len, const uint8_t* hash, size_t hash_len, uint8_t out[96]) {
+int ovh_sign(ovh_ctx* c, const uint8_t* key, size_t key_len, const uint8_t* hash, size_t hash_len, uint8_t out[96]) {
   if (!c || !out) return OVH_ERR_ARG;
   if (hash_len != 32 || !hash) return OVH_ERR_HASH_LEN;
-  if (!sk_valid(sk, sk_len)) return BLST_BAD_ENCODING;
+  uint8_t sk[32];
+  CHK(sk_parse(c, key, key_len, sk));
+  c = pick_sub(c);
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  if (ensure_in(c, 256)) return OVH_ERR_DEVICE;
+  CHK(ensure_in(c, 256));
   HIPCHK(hipMemcpyAsync(c->in_buf, sk, 32, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->in_buf + 32, hash, 32, hipMemcpyHostToDevice, c->stream));
   k_sign<<<1, WG, 0, c->stream>>>(1, c->in_buf, c->in_buf + 32, c->xmd, c->in_buf + 64);
@@ -861,12 +1481,14 @@ int ovh_sign(ovh_ctx* c, const uint8_t* sk, size_t sk_len, const uint8_t* hash, 
   return 0;
 }
 
-int ovh_sk_to_pk(ovh_ctx* c, const uint8_t* sk, size_t sk_len, uint8_t out[48]) {
+int ovh_sk_to_pk(ovh_ctx* c, const uint8_t* key, size_t key_len, uint8_t out[48]) {
   if (!c || !out) return OVH_ERR_ARG;
-  if (!sk_valid(sk, sk_len)) return BLST_BAD_ENCODING;
+  uint8_t sk[32];
+  CHK(sk_parse(c, key, key_len, sk));
+  c = pick_sub(c);
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  if (ensure_in(c, 128)) return OVH_ERR_DEVICE;
+  CHK(ensure_in(c, 128));
   HIPCHK(hipMemcpyAsync(c->in_buf, sk, 32, hipMemcpyHostToDevice, c->stream));
   k_sk_to_pk<<<1, WG, 0, c->stream>>>(1, c->in_buf, c->in_buf + 32);
   HIPCHK(hipGetLastError());
@@ -880,19 +1502,48 @@ int ovh_verify(ovh_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* ha
   if (!c) return OVH_ERR_ARG;
   if (hash_len != 32 || !hash) return OVH_ERR_HASH_LEN;
   if (sig_len > 4096 || pk_len > 4096 || (sig_len && !sig) || (pk_len && !pk)) return OVH_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
-  if (ensure_in(c, 32 + sig_len + pk_len + 64)) return OVH_ERR_DEVICE;
-  uint8_t* d = c->in_buf;
-  HIPCHK(hipMemcpyAsync(d, hash, 32, hipMemcpyHostToDevice, c->stream));
-  if (sig_len) HIPCHK(hipMemcpyAsync(d + 32, sig, sig_len, hipMemcpyHostToDevice, c->stream));
-  if (pk_len) HIPCHK(hipMemcpyAsync(d + 32 + sig_len, pk, pk_len, hipMemcpyHostToDevice, c->stream));
-  k_verify_one<<<1, WG, 0, c->stream>>>(d + 32, (uint32_t)sig_len, d, 32, d + 32 + sig_len, (uint32_t)pk_len, c->xmd,
-                                         c->result);
+  const bool fixed = sig_len == 96 && pk_len == 48;
+  int32_t code;
+  if (fixed && cache_get(c, sig, hash, pk, &code)) return code;
+  ovh_ctx* s = pick_sub(c);
+  std::lock_guard<std::mutex> g(s->mu);
+  HIPCHK(hipSetDevice(s->device));
+  if (fixed) {
+    // the batch path at n = 1 (the Fp-VM vote program + final check): its combined check is the
+    // vote's own pairing check, so a failed verdict with a clean parse is VERIFY_FAIL
+    uint8_t* d;
+    CHK(stage_batch(s, 1, sig, hash, pk, &d));
+    int32_t* dc = (int32_t*)(d + 176);
+    std::vector<int32_t> idx;
+    KeySrc key{d + 128, PkSrc{}};
+    if (table_lookup(s, 1, pk, idx)) {
+      HIPCHK(hipMemcpyAsync(dc + 1, idx.data(), 4, hipMemcpyHostToDevice, s->stream));
+      key = KeySrc{nullptr, PkSrc{s->tab.planes, s->tab.cap, s->tab.flags, dc + 1}};
+    }
+    CHK(ensure_cap(s, 1));
+    int slot;
+    CHK(take_slot(s, &slot));
+    CHK(batch_front(s, slot, 1, d, d + 96, key, dc, false));
+    enqueue_final(s, s->stream, region_F(s, slot, 1), region_S(s, slot, 1), 1, s->result);
+    HIPCHK(hipGetLastError());
+    int32_t out[2] = {-1, -1};
+    HIPCHK(hipMemcpyAsync(&out[0], dc, 4, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipMemcpyAsync(&out[1], s->result, 4, hipMemcpyDeviceToHost, s->stream));
+    HIPCHK(hipStreamSynchronize(s->stream));
+    return out[0] != 0 ? out[0] : (out[1] == 1 ? 0 : BLST_VERIFY_FAIL);
+  }
+  // other encodings (uncompressed keys / signatures, wrong lengths): the single-lane kernel
+  CHK(ensure_in(s, 32 + sig_len + pk_len + 64));
+  uint8_t* d = s->in_buf;
+  HIPCHK(hipMemcpyAsync(d, hash, 32, hipMemcpyHostToDevice, s->stream));
+  if (sig_len) HIPCHK(hipMemcpyAsync(d + 32, sig, sig_len, hipMemcpyHostToDevice, s->stream));
+  if (pk_len) HIPCHK(hipMemcpyAsync(d + 32 + sig_len, pk, pk_len, hipMemcpyHostToDevice, s->stream));
+  k_verify_one<<<1, WG, 0, s->stream>>>(d + 32, (uint32_t)sig_len, d, 32, d + 32 + sig_len, (uint32_t)pk_len, s->xmd,
+                                         s->result);
   HIPCHK(hipGetLastError());
   int32_t r = -1;
-  HIPCHK(hipMemcpyAsync(&r, c->result, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpyAsync(&r, s->result, 4, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
   return r;
 }
 
@@ -910,7 +1561,7 @@ static int stage_list(ovh_ctx* c, const uint8_t* data, const size_t* lens, size_
   }
   const size_t data_bytes = (total + 15) & ~(size_t)15;
   const size_t need = base + data_bytes + 16 * (n + 1);
-  if (ensure_in(c, need)) return OVH_ERR_DEVICE;
+  if (need > c->in_cap) return OVH_ERR_ARG;  // callers size the staging buffer first
   uint8_t* d = c->in_buf + base;
   if (total) HIPCHK(hipMemcpyAsync(d, data, total, hipMemcpyHostToDevice, c->stream));
   uint64_t* m = (uint64_t*)(d + data_bytes);
@@ -922,42 +1573,40 @@ static int stage_list(ovh_ctx* c, const uint8_t* data, const size_t* lens, size_
   return 0;
 }
 
+static size_t list_bytes(const size_t* lens, size_t n) {
+  size_t t = 0;
+  for (size_t i = 0; i < n; ++i) t += lens[i];
+  return t;
+}
+
 int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, size_t n_sigs, const uint8_t* pks,
                        const size_t* pk_lens, size_t n_pks, uint8_t out[96]) {
   if (!c || !out) return OVH_ERR_ARG;
   if (n_sigs != n_pks) return OVH_ERR_LEN_MISMATCH;
   const size_t n = n_sigs;
   if (n && (!sig_lens || !pk_lens)) return OVH_ERR_ARG;
+  c = pick_sub(c);
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  if (drain(c) || ensure_cap(c, n > 0 ? n : 1)) return OVH_ERR_DEVICE;
-  // the staging buffer may be reallocated by the second stage_list: stage both first, then launch
+  CHK(ensure_scr(c, n > 0 ? n : 1));
+  CHK(ensure_in(c, list_bytes(sig_lens, n) + list_bytes(pk_lens, n) + 512 + 32 * (n + 1)));
   uint8_t *ds, *dp;
   uint64_t *so, *sl, *po, *pl;
   size_t used1 = 0, used2 = 0;
-  {
-    // size the staging buffer for both lists up front
-    size_t t1 = 0, t2 = 0;
-    for (size_t i = 0; i < n; ++i) {
-      t1 += sig_lens[i];
-      t2 += pk_lens[i];
-    }
-    if (ensure_in(c, t1 + t2 + 512 + 32 * (n + 1))) return OVH_ERR_DEVICE;
-  }
-  if (stage_list(c, sigs, sig_lens, n, 0, &ds, &so, &sl, &used1)) return OVH_ERR_DEVICE;
-  if (stage_list(c, pks, pk_lens, n, used1, &dp, &po, &pl, &used2)) return OVH_ERR_DEVICE;
-  Slab pts{c->state, c->cap};
-  Slab ppts{c->state + (size_t)6 * 12 * c->cap, c->cap};
+  CHK(stage_list(c, sigs, sig_lens, n, 0, &ds, &so, &sl, &used1));
+  CHK(stage_list(c, pks, pk_lens, n, used1, &dp, &po, &pl, &used2));
+  Slab pts{c->scr, c->scr_cap};
+  Slab ppts{c->scr + (size_t)6 * 12 * c->scr_cap, c->scr_cap};
   if (n) {
-    k_parse_sig_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, ds, so, sl, (c->flags & OVH_FLAG_AGG_NO_GROUPCHECK) ? 0 : 1,
-                                                   c->st_sig, pts);
-    k_parse_pk_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, dp, po, pl, c->st_pk, ppts);
+    k_parse_sig_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, ds, so, sl,
+                                                   (c->flags & OVH_FLAG_AGG_NO_GROUPCHECK) ? 0 : 1, c->scr_sig, pts);
+    k_parse_pk_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, dp, po, pl, c->scr_pk, ppts);
     HIPCHK(hipGetLastError());
   }
   std::vector<int32_t> cs(n), cp(n);
   if (n) {
-    HIPCHK(hipMemcpyAsync(cs.data(), c->st_sig, 4 * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipMemcpyAsync(cp.data(), c->st_pk, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(cs.data(), c->scr_sig, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(cp.data(), c->scr_pk, 4 * n, hipMemcpyDeviceToHost, c->stream));
   }
   HIPCHK(hipStreamSynchronize(c->stream));
   // consensus.rs:431-439: per pair, signature first, then the public key.
@@ -976,24 +1625,24 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
   return 0;
 }
 
-// Parses + sums a pk list on the device; the Jacobian sum (36 words) stays at *d_sum.
-static int sum_pks(ovh_ctx* c, const uint8_t* pks, const size_t* pk_lens, size_t n, uint8_t* out48, uint32_t** d_sum) {
+// Parses + sums a pk list on the device; the Jacobian sum (36 words) stays at *d_sum (in the
+// staging buffer, after `reserve` bytes kept free for the caller). Caller holds c->mu.
+static int sum_pks(ovh_ctx* c, const uint8_t* pks, const size_t* pk_lens, size_t n, size_t reserve, uint8_t* out48,
+                   uint32_t** d_sum) {
   if (n && !pk_lens) return OVH_ERR_ARG;
-  if (drain(c) || ensure_cap(c, n > 0 ? n : 1)) return OVH_ERR_DEVICE;
-  size_t t = 0;
-  for (size_t i = 0; i < n; ++i) t += pk_lens[i];
-  if (ensure_in(c, t + 16 * (n + 1) + 256)) return OVH_ERR_DEVICE;
+  CHK(ensure_scr(c, n > 0 ? n : 1));
+  CHK(ensure_in(c, list_bytes(pk_lens, n) + 16 * (n + 1) + 512 + reserve));
   uint8_t* dp;
   uint64_t *po, *pl;
   size_t used = 0;
-  if (stage_list(c, pks, pk_lens, n, 0, &dp, &po, &pl, &used)) return OVH_ERR_DEVICE;
-  Slab ppts{c->state, c->cap};
+  CHK(stage_list(c, pks, pk_lens, n, 0, &dp, &po, &pl, &used));
+  Slab ppts{c->scr, c->scr_cap};
   if (n) {
-    k_parse_pk_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, dp, po, pl, c->st_pk, ppts);
+    k_parse_pk_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, dp, po, pl, c->scr_pk, ppts);
     HIPCHK(hipGetLastError());
   }
   std::vector<int32_t> cp(n);
-  if (n) HIPCHK(hipMemcpyAsync(cp.data(), c->st_pk, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  if (n) HIPCHK(hipMemcpyAsync(cp.data(), c->scr_pk, 4 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   for (size_t i = 0; i < n; ++i)
     if (cp[i] != BLST_SUCCESS) return OVH_ERR_PUBKEY;
@@ -1010,27 +1659,18 @@ static int sum_pks(ovh_ctx* c, const uint8_t* pks, const size_t* pk_lens, size_t
 
 int ovh_aggregate_pks(ovh_ctx* c, const uint8_t* pks, const size_t* pk_lens, size_t n, uint8_t out[48]) {
   if (!c || !out) return OVH_ERR_ARG;
+  c = pick_sub(c);
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   uint32_t* sum = nullptr;
-  return sum_pks(c, pks, pk_lens, n, out, &sum);
+  return sum_pks(c, pks, pk_lens, n, 0, out, &sum);
 }
 
-int ovh_verify_aggregated(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, const uint8_t* hash, size_t hash_len,
-                          const uint8_t* pks, const size_t* pk_lens, size_t n) {
-  if (!c) return OVH_ERR_ARG;
-  if (agg_len > 4096 || (agg_len && !agg_sig)) return OVH_ERR_ARG;
-  if (n && !pk_lens) return OVH_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
+static int verify_aggregated_locked(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, const uint8_t* hash,
+                                    size_t hash_len, const uint8_t* pks, const size_t* pk_lens, size_t n) {
   HIPCHK(hipSetDevice(c->device));
-  {
-    size_t t = 0;
-    for (size_t i = 0; i < n; ++i) t += pk_lens[i];
-    if (ensure_in(c, t + 16 * (n + 1) + 1024 + agg_len)) return OVH_ERR_DEVICE;  // no realloc below
-  }
   uint32_t* sum = nullptr;
-  int e = sum_pks(c, pks, pk_lens, n, nullptr, &sum);
-  if (e) return e;
+  CHK(sum_pks(c, pks, pk_lens, n, 1024 + agg_len, nullptr, &sum));
   // stage sig + hash behind the sum (sum occupies 36 words + 48 bytes)
   uint8_t* d = (uint8_t*)sum + 256;
   const size_t hl = (hash && hash_len <= 64) ? hash_len : 0;
@@ -1045,130 +1685,282 @@ int ovh_verify_aggregated(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, co
   return r;
 }
 
-// ---- batch ----
-// Per-vote stages of a batch on the main stream: hash_to_field, then the vote kernel with fold
-// level 0 fused in: *outF / *outS = ceil(n / 4) partials as planes in the slot's fold scratch
-// (half 0), *out_m their count.
-static int batch_front(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
-                       uint64_t seed, int32_t* d_codes, Slab* outF, Slab* outS, uint32_t* out_m, int slot = -1) {
-  Slab s{c->state, c->cap};
-  hipStream_t st = c->stream;
-  c->ev_mask = 0;
-  const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
-  Slab p0{c->red, c->red_cap};
-  if (slot >= 0) {
-    // pipelined: hash_to_field on its own stream, as soon as the slot's previous batch has
-    // finished its per-vote stages (the only reader of the S_U planes), so it runs beside the
-    // current vote kernel; the vote waits for it
-    HIPCHK(hipStreamWaitEvent(c->hstream, c->ev_front[slot], 0));
-    {
-      StageScope p(c, ST_H2F, c->hstream);
-      k_h2f<<<nblk(n), WG, 0, c->hstream>>>(n, d_hashes, c->xmd, s);
-    }
-    HIPCHK(hipEventRecord(c->ev_h[slot], c->hstream));
-    HIPCHK(hipStreamWaitEvent(st, c->ev_h[slot], 0));
-  } else {
-    StageScope p(c, ST_H2F);
-    k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s);
+int ovh_verify_aggregated(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, const uint8_t* hash, size_t hash_len,
+                          const uint8_t* pks, const size_t* pk_lens, size_t n) {
+  if (!c) return OVH_ERR_ARG;
+  if (agg_len > 4096 || (agg_len && !agg_sig)) return OVH_ERR_ARG;
+  if (n && !pk_lens) return OVH_ERR_ARG;
+  c = pick_sub(c);
+  std::lock_guard<std::mutex> g(c->mu);
+  return verify_aggregated_locked(c, agg_sig, agg_len, hash, hash_len, pks, pk_lens, n);
+}
+
+static int set_validators_locked(ovh_ctx* c, const uint8_t* pks, size_t n) {
+  HIPCHK(hipSetDevice(c->device));
+  CHK(sync_all(c));
+  ValidatorTable& t = c->tab;
+  uint32_t cap = 64;
+  while (cap < n) cap <<= 1;
+  if (cap > t.cap || !t.planes) {
+    for (void* p : {(void*)t.planes, (void*)t.flags})
+      if (p) (void)hipFree(p);
+    t.planes = nullptr;
+    t.flags = nullptr;
+    t.cap = 0;
+    HIPCHK(hipMalloc(&t.planes, (size_t)3 * 12 * cap * 4));
+    HIPCHK(hipMalloc(&t.flags, (size_t)cap * 4));
+    t.cap = cap;
   }
-  {
-    StageScope p(c, ST_VOTE);
-    k_vm_vote<<<nwg, 64, LDS_VOTE, st>>>(n, c->vm_vote, c->vm_fold, c->vm_consts, d_pks, d_sigs, s, seed, d_codes,
-                                         p0);
+  t.n = 0;
+  t.keys.clear();
+  t.index.clear();
+  t.sorted.clear();
+  t.hflags.assign(n, 0);
+  if (n) {
+    CHK(ensure_in(c, n * 48 + 64));
+    HIPCHK(hipMemcpyAsync(c->in_buf, pks, n * 48, hipMemcpyHostToDevice, c->stream));
+    k_table_build<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, c->in_buf, Slab{t.planes, t.cap}, t.flags);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(t.hflags.data(), t.flags, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
   }
-  HIPCHK(hipGetLastError());
-  c->last_n = n;
-  *outF = p0;
-  *outS = Slab{c->red + (size_t)12 * 12 * c->red_cap, c->red_cap};
-  *out_m = nwg;
+  for (size_t i = 0; i < n; ++i) {
+    t.keys.emplace_back((const char*)pks + 48 * i, 48);
+    t.index.emplace(t.keys.back(), (uint32_t)i);  // keeps the first of duplicate keys
+    t.sorted.push_back((uint32_t)i);
+  }
+  std::stable_sort(t.sorted.begin(), t.sorted.end(), [&](uint32_t a, uint32_t b) { return t.keys[a] < t.keys[b]; });
+  t.n = (uint32_t)n;
   return 0;
 }
 
-// Fold levels down to <= `until` partials, on stream st, ping-ponging through the slot's fold
-// scratch (the level-0 partials are in half 0; *flip_io carries the next output half across
-// calls). slices = 4 (main stream) or 1 (the final stream, beside the next batch's vote
-// workgroups).
-static int fold_levels(ovh_ctx* c, hipStream_t st, int slices, Slab* F, Slab* S, uint32_t* m, uint32_t until = 4,
-                       int* flip_io = nullptr) {
-  StageScope p(c, ST_FOLD, st);
-  int flip = flip_io ? *flip_io : 1;
-  while (*m > until) {
-    const uint32_t mo = (*m + 3) / 4;
-    uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
-    Slab o{base, c->red_cap};
-    if (slices == 1)
-      k_vm_fold<1><<<mo, 64, LDS_FOLD1, st>>>(*m, c->vm_fold, c->vm_consts, *F, *S, o, nullptr);
-    else
-      k_vm_fold<VM_FOLD_UNITS><<<(mo + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(*m, c->vm_fold, c->vm_consts, *F,
-                                                                                 *S, o, nullptr);
-    *F = o;
-    *S = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
-    *m = mo;
-    flip ^= 1;
+int ovh_set_validators(ovh_ctx* c, const uint8_t* pks, size_t n) {
+  if (!c || (n && !pks) || n > (1u << 20)) return OVH_ERR_ARG;
+  if (!c->sub.empty()) {
+    for (ovh_ctx* s : c->sub) {
+      std::lock_guard<std::mutex> g(s->mu);
+      CHK(set_validators_locked(s, pks, n));
+    }
+    std::lock_guard<std::mutex> g(c->mu);
+    c->tab.n = (uint32_t)n;
+    c->tab.keys = c->sub[0]->tab.keys;
+    c->tab.hflags = c->sub[0]->tab.hflags;
+    c->tab.sorted = c->sub[0]->tab.sorted;
+    return 0;
   }
-  if (flip_io) *flip_io = flip;
-  return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
+  std::lock_guard<std::mutex> g(c->mu);
+  return set_validators_locked(c, pks, n);
 }
 
-// Verdict words in c->result: [0] single-call APIs, then per batch slot the pipelined batch
-// and pipelined combine verdicts, then the synchronous combine's.
-enum { RES_BATCH = 4, RES_COMBINE = RES_BATCH + OVH_BATCH_SLOTS, RES_SYNC = RES_COMBINE + OVH_BATCH_SLOTS };
-static_assert(RES_SYNC < 16, "verdict words fit c->result");
+int ovh_verify_batch(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                     int32_t* codes) {
+  if (!c || (n && (!sigs || !hashes || !pks || !codes))) return OVH_ERR_ARG;
+  if (n == 0) return 0;
+  if (n > (1u << 24)) return OVH_ERR_ARG;
+  if (!c->sub.empty()) return verify_host_multi(c, n, sigs, hashes, pks, codes);
+  std::lock_guard<std::mutex> g(c->mu);
+  return verify_host_locked(c, n, sigs, hashes, pks, codes);
+}
 
-int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
-                             uint64_t seed, int32_t* d_codes, uint8_t* d_partial) {
-  if (!c || !d_codes || !d_partial || (n && (!d_sigs || !d_hashes || !d_pks))) return OVH_ERR_ARG;
+int ovh_prefetch(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks) {
+  if (!c || (n && (!sigs || !hashes || !pks))) return OVH_ERR_ARG;
+  if (n == 0) return 0;
+  std::vector<int32_t> codes(n);
+  CHK(ovh_verify_batch(c, n, sigs, hashes, pks, codes.data()));
+  cache_put(c, n, sigs, hashes, pks, codes.data());
+  return 0;
+}
+
+int ovh_cache_config(ovh_ctx* c, size_t capacity) {
+  if (!c) return OVH_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->cache.mu);
+  c->cache.cap = capacity;
+  while (c->cache.map.size() > capacity && !c->cache.fifo.empty()) {
+    c->cache.map.erase(c->cache.fifo.front());
+    c->cache.fifo.pop_front();
+  }
+  return 0;
+}
+
+int ovh_cache_stats(ovh_ctx* c, uint64_t stats[3]) {
+  if (!c || !stats) return OVH_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->cache.mu);
+  stats[0] = c->cache.hits;
+  stats[1] = c->cache.misses;
+  stats[2] = c->cache.map.size();
+  return 0;
+}
+
+static int qc_batch_locked(ovh_ctx* c, size_t nq, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* bitmaps,
+                           size_t bitmap_len, int32_t* codes) {
+  HIPCHK(hipSetDevice(c->device));
+  const ValidatorTable& t = c->tab;
+  // voters per QC (extract_voters: bit k MSB-first <-> k-th key in sorted order; zip truncates)
+  const size_t nbits = bitmap_len * 8 < t.n ? bitmap_len * 8 : t.n;
+  std::vector<uint32_t> off(1, 0), ent;
+  std::vector<size_t> dev;  // QCs that go to the device batch
+  for (size_t q = 0; q < nq; ++q) {
+    const uint8_t* bm = bitmaps + q * bitmap_len;
+    uint32_t fl = 0, cnt = 0;
+    const size_t start = ent.size();
+    for (size_t k = 0; k < nbits; ++k)
+      if ((bm[k / 8] >> (7 - k % 8)) & 1) {
+        const uint32_t e = t.sorted[k];
+        ent.push_back(e);
+        fl |= t.hflags[e];
+        ++cnt;
+      }
+    // consensus.rs:454-458 (key parse) -> :371 (empty aggregate) -> ...
+    if (fl & PKF_PARSE) {
+      codes[q] = OVH_ERR_PUBKEY;
+      ent.resize(start);
+    } else if (!cnt) {
+      codes[q] = BLST_AGGR_TYPE_MISMATCH;
+    } else if (fl & PKF_GRP) {
+      // a key outside G1: the sum's own group check decides -> the exact single-QC path
+      std::vector<uint8_t> cat;
+      std::vector<size_t> lens;
+      for (size_t k = start; k < ent.size(); ++k) {
+        cat.insert(cat.end(), t.keys[ent[k]].begin(), t.keys[ent[k]].end());
+        lens.push_back(48);
+      }
+      ent.resize(start);
+      const int r = verify_aggregated_locked(c, sigs + 96 * q, 96, hashes + 32 * q, 32, cat.data(), lens.data(), cnt);
+      if (r >= OVH_ERR_ARG) return r;
+      codes[q] = r;
+    } else {
+      dev.push_back(q);
+      off.push_back((uint32_t)ent.size());
+    }
+  }
+  const size_t nd = dev.size();
+  if (!nd) return 0;
+  // device batch: apk per QC -> vote_t over (sig, hash, apk)
+  if (nd > c->qc_cap || !c->qc_buf) {
+    if (c->qc_buf) (void)hipFree(c->qc_buf);
+    c->qc_buf = nullptr;
+    c->qc_cap = 0;
+    uint32_t cap = 64;
+    while (cap < nd) cap <<= 1;
+    HIPCHK(hipMalloc(&c->qc_buf, (size_t)(3 * 12 + 1) * cap * 4));
+    c->qc_cap = cap;
+  }
+  const size_t bytes = nd * (96 + 32 + 4) + off.size() * 4 + ent.size() * 4 + 256;
+  CHK(ensure_in(c, bytes));
+  uint8_t* d = c->in_buf;
+  std::vector<uint8_t> hs(nd * 96), hh(nd * 32);
+  for (size_t j = 0; j < nd; ++j) {
+    memcpy(&hs[96 * j], sigs + 96 * dev[j], 96);
+    memcpy(&hh[32 * j], hashes + 32 * dev[j], 32);
+  }
+  int32_t* dc = (int32_t*)(d + nd * 128);
+  uint32_t* doff = (uint32_t*)(dc + nd);
+  uint32_t* dent = doff + off.size();
+  HIPCHK(hipMemcpyAsync(d, hs.data(), nd * 96, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(d + nd * 96, hh.data(), nd * 32, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(doff, off.data(), off.size() * 4, hipMemcpyHostToDevice, c->stream));
+  if (!ent.empty()) HIPCHK(hipMemcpyAsync(dent, ent.data(), ent.size() * 4, hipMemcpyHostToDevice, c->stream));
+  uint32_t* qflags = c->qc_buf + (size_t)3 * 12 * c->qc_cap;
+  k_qc_apk<<<nblk(nd), WG, 0, c->stream>>>((uint32_t)nd, doff, dent, Slab{t.planes, t.cap},
+                                          Slab{c->qc_buf, c->qc_cap}, qflags);
+  HIPCHK(hipGetLastError());
+  CHK(verify_async_locked(c, nd, d, d + nd * 96, KeySrc{nullptr, PkSrc{c->qc_buf, c->qc_cap, qflags, nullptr}}, dc));
+  CHK(sync_all(c));
+  std::vector<int32_t> dcodes(nd);
+  HIPCHK(hipMemcpyAsync(dcodes.data(), dc, 4 * nd, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (size_t j = 0; j < nd; ++j) codes[dev[j]] = dcodes[j];
+  return 0;
+}
+
+int ovh_verify_qc_batch(ovh_ctx* c, size_t nq, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* bitmaps,
+                        size_t bitmap_len, int32_t* codes) {
+  if (!c || (nq && (!sigs || !hashes || !codes || (bitmap_len && !bitmaps)))) return OVH_ERR_ARG;
+  if (nq == 0) return 0;
+  if (nq > (1u << 20)) return OVH_ERR_ARG;
+  ovh_ctx* s = c->sub.empty() ? c : c->sub[0];
+  std::lock_guard<std::mutex> g(s->mu);
+  if (!s->tab.n) return OVH_ERR_ARG;
+  return qc_batch_locked(s, nq, sigs, hashes, bitmaps, bitmap_len, codes);
+}
+
+int ovh_set_test_rlc(ovh_ctx* c, uint64_t seed, uint64_t index_base) {
+  if (!c || !(c->flags & OVH_FLAG_TEST_RLC)) return OVH_ERR_ARG;
+  for (ovh_ctx* s : c->sub) {
+    std::lock_guard<std::mutex> g(s->mu);
+    s->test_seed = seed;
+    s->test_base = index_base;
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  c->test_seed = seed;
+  c->test_base = index_base;
+  return 0;
+}
+
+int ovh_verify_batch_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
+                                  const uint8_t* d_pks, int32_t* d_codes) {
+  if (!c || !c->sub.empty() || (n && (!d_sigs || !d_hashes || !d_pks || !d_codes))) return OVH_ERR_ARG;
+  if (n == 0) return 0;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
+  return verify_async_locked(c, n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes);
+}
+
+int ovh_batch_wait(ovh_ctx* c) {
+  if (!c || !c->sub.empty()) return OVH_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  return sync_all(c);
+}
+
+int ovh_verify_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
+                            int32_t* d_codes) {
+  if (!c || !c->sub.empty() || (n && (!d_sigs || !d_hashes || !d_pks || !d_codes))) return OVH_ERR_ARG;
+  if (n == 0) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  CHK(verify_async_locked(c, n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes));
+  return sync_all(c);
+}
+
+int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
+                             int32_t* d_codes, uint8_t* d_partial, void* stream) {
+  if (!c || !c->sub.empty() || !d_codes || !d_partial || (n && (!d_sigs || !d_hashes || !d_pks))) return OVH_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  hipStream_t st = (hipStream_t)stream;
   if (n == 0) {
     // neutral partial: F = 1, S = O = (0 : 1 : 0)
-    std::vector<uint32_t> p(216, 0);
-    for (int k = 0; k < 12; ++k) p[k] = ONE_M[k];
-    for (int k = 0; k < 12; ++k) p[144 + 24 + k] = ONE_M[k];  // Y.c0 = 1
-    HIPCHK(hipMemcpyAsync(d_partial, p.data(), 864, hipMemcpyHostToDevice, c->stream));
+    static uint32_t neutral[216];
+    for (int k = 0; k < 12; ++k) neutral[k] = ONE_M[k];
+    for (int k = 0; k < 12; ++k) neutral[144 + 24 + k] = ONE_M[k];  // Y.c0 = 1
+    if (st) {
+      HIPCHK(hipEventRecord(c->ev_x[0], st));
+      HIPCHK(hipStreamWaitEvent(c->stream, c->ev_x[0], 0));
+    }
+    HIPCHK(hipMemcpyAsync(d_partial, neutral, 864, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->last_n = 0;
     return 0;
   }
-  if (ensure_cap(c, n)) return OVH_ERR_DEVICE;
-  if (take_slot(c, (int)(c->pipe_k++ % OVH_BATCH_SLOTS))) return OVH_ERR_DEVICE;
-  Slab F, S;
-  uint32_t m;
-  int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m);
-  if (e || (e = fold_levels(c, c->stream, VM_SLICES, &F, &S, &m))) return e;
-  if (m > 1) {  // fold the last <= 4 into one partial
-    uint32_t* base = c->red + (size_t)(F.p == c->red ? 1 : 0) * PART_PLANES * 12 * c->red_cap;
-    Slab o{base, c->red_cap};
-    k_vm_fold<VM_FOLD_UNITS><<<1, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts, F, S, o, nullptr);
-    F = o;
+  CHK(ensure_cap(c, n));
+  int slot;
+  CHK(take_slot(c, &slot));
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false));
+  CHK(shard_partial(c, slot, (uint32_t)n, (uint32_t*)d_partial, st));
+  if (st) {
+    HIPCHK(hipEventRecord(c->ev_x[1], c->stream));
+    HIPCHK(hipStreamWaitEvent(st, c->ev_x[1], 0));
+    return 0;
   }
-  // pack element 0 (F planes, S planes) into the AoS partial
-  k_pack_partial2<<<1, 64, 0, c->stream>>>(F, m > 1 ? Slab{F.p + (size_t)12 * 12 * F.cap, F.cap} : S,
-                                           (uint32_t*)d_partial);
-  HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
 
-// Final check on <= 4 partials given as planes: k_vm_final on stream `st`, verdict to *d_res.
-static void enqueue_final(ovh_ctx* c, hipStream_t st, Slab F, Slab S, uint32_t m, int32_t* d_res) {
-  StageScope p(c, ST_FINAL, st);
-  k_vm_final<<<1, 64, LDS_FINAL, st>>>(m, c->vm_final, c->vm_consts, F, S, d_res);
-}
-
-// Per-vote fallback of the batch in state slot `slot`, on stream `st`, skipped on the device
-// when *d_verdict == 1 (d_verdict null: always runs).
-static void enqueue_fallback(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, int32_t* d_codes,
-                             const int32_t* d_verdict) {
-  StageScope p(c, ST_FALLBACK, st);
-  k_vm_pairchk<<<(n + VM_SLICES - 1) / VM_SLICES, 64, LDS_PAIRCHK, st>>>(
-      n, c->vm_pairchk, c->vm_consts, Slab{c->state_slot[slot], c->cap}, d_codes, d_verdict);
-}
-
-// AoS partials (k <= 16) -> <= 4 partials as planes in the fin area of `slot` (unpack, and one
-// fold level when k > 4), on stream st. Scratch: fin slot area + the slot's upper half.
-static int stage_partials(ovh_ctx* c, hipStream_t st, size_t k, const uint8_t* d_partials, uint32_t* scratch,
-                          Slab* F, Slab* S, uint32_t* m) {
+// AoS partials (k <= 16) -> <= 4 partials as planes in `scratch` (unpack, and one fold level
+// when k > 4), on stream st.
+static int stage_partials(ovh_ctx* c, hipStream_t st, size_t k, const uint8_t* d_partials, uint32_t* scratch, Slab* F,
+                          Slab* S, uint32_t* m) {
   Slab uF{scratch, 16}, uS{scratch + (size_t)12 * 12 * 16, 16};
   k_unpack_partials<<<(uint32_t)((k * PART_PLANES + 63) / 64), 64, 0, st>>>((uint32_t)k, (const uint32_t*)d_partials,
                                                                            uF, uS);
@@ -1178,148 +1970,96 @@ static int stage_partials(ovh_ctx* c, hipStream_t st, size_t k, const uint8_t* d
     *m = (uint32_t)k;
   } else {
     uint32_t* o = scratch + (size_t)PART_PLANES * 12 * 16;
-    Slab oF{o, 4};
-    k_vm_fold<VM_FOLD_UNITS><<<1, 64, LDS_FOLD, st>>>((uint32_t)k, c->vm_fold, c->vm_consts, uF, uS, oF, nullptr);
-    *F = oF;
+    *F = Slab{o, 4};
     *S = Slab{o + (size_t)12 * 12 * 4, 4};
+    k_vm_fold<VM_FOLD_UNITS><<<1, 64, LDS_FOLD, st>>>((uint32_t)k, c->vm_fold, c->vm_consts, uF, uS, *F, nullptr);
     *m = (uint32_t)((k + 3) / 4);
   }
   return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
 }
 
-int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials) {
-  if (!c || !d_partials || k == 0 || k > 4096) return -OVH_ERR_ARG;
+int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials, int32_t* verdict) {
+  if (!c || !c->sub.empty() || !d_partials || !verdict || k == 0 || k > 4096) return OVH_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  if (hipSetDevice(c->device) != hipSuccess) return -OVH_ERR_DEVICE;
-  if (ensure_cap(c, k * 4 > 256 ? k * 4 : 256)) return -OVH_ERR_DEVICE;
-  if (drain(c)) return -OVH_ERR_DEVICE;
-  // AoS partials -> planes (F at S_F, S at S_RS of the current slot's state), fold to <= 4
-  Slab F{c->state + (size_t)S_F * 12 * c->cap, c->cap}, S{c->state + (size_t)S_RS * 12 * c->cap, c->cap};
+  HIPCHK(hipSetDevice(c->device));
+  // own scratch (never the batch slots): U = k partials, then two ping-pong regions of k / 4
+  const uint32_t kc = (uint32_t)((k + 15) & ~(size_t)15);
+  if (kc > c->comb_cap || !c->comb) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->comb) (void)hipFree(c->comb);
+    c->comb = nullptr;
+    c->comb_cap = 0;
+    HIPCHK(hipMalloc(&c->comb, (size_t)3 * PART_PLANES * 12 * kc * 4));
+    c->comb_cap = kc;
+  }
+  auto regF = [&](int r) { return Slab{c->comb + (size_t)r * PART_PLANES * 12 * c->comb_cap, c->comb_cap}; };
+  auto regS = [&](int r) {
+    return Slab{c->comb + (size_t)r * PART_PLANES * 12 * c->comb_cap + (size_t)12 * 12 * c->comb_cap, c->comb_cap};
+  };
   k_unpack_partials<<<(uint32_t)((k * PART_PLANES + 63) / 64), 64, 0, c->stream>>>((uint32_t)k,
-                                                                                   (const uint32_t*)d_partials, F, S);
+                                                                                   (const uint32_t*)d_partials, regF(0),
+                                                                                   regS(0));
   uint32_t m = (uint32_t)k;
-  int flip = 0;
+  int reg = 0;
   while (m > 4) {
     const uint32_t mo = (m + 3) / 4;
-    uint32_t* base = c->red + (size_t)flip * PART_PLANES * 12 * c->red_cap;
-    Slab o{base, c->red_cap};
-    k_vm_fold<VM_FOLD_UNITS><<<(mo + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, c->stream>>>(m, c->vm_fold, c->vm_consts,
-                                                                                       F, S, o, nullptr);
-    F = o;
-    S = Slab{base + (size_t)12 * 12 * c->red_cap, c->red_cap};
+    const int ro = reg == 1 ? 2 : 1;
+    k_vm_fold<VM_FOLD_UNITS><<<(mo + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, c->stream>>>(
+        m, c->vm_fold, c->vm_consts, regF(reg), regS(reg), regF(ro), nullptr);
+    reg = ro;
     m = mo;
-    flip ^= 1;
   }
-  enqueue_final(c, c->stream, F, S, m, c->result + RES_SYNC);
-  if (hipGetLastError() != hipSuccess) return -OVH_ERR_DEVICE;
+  enqueue_final(c, c->stream, regF(reg), regS(reg), m, c->result + RES_SYNC);
+  HIPCHK(hipGetLastError());
   int32_t r = -1;
-  if (hipMemcpyAsync(&r, c->result + RES_SYNC, 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-      hipStreamSynchronize(c->stream) != hipSuccess)
-    return -OVH_ERR_DEVICE;
-  return r;
+  HIPCHK(hipMemcpyAsync(&r, c->result + RES_SYNC, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *verdict = r == 1 ? 1 : 0;
+  return 0;
 }
 
 int ovh_batch_fallback_device(ovh_ctx* c, size_t n, int32_t* d_codes) {
-  if (!c || !d_codes) return OVH_ERR_ARG;
+  if (!c || !c->sub.empty() || !d_codes) return OVH_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return 0;
-  if (n != c->last_n) return OVH_ERR_ARG;
-  enqueue_fallback(c, c->stream, c->last_slot, (uint32_t)n, d_codes, nullptr);
+  if (n != c->last_n || c->slot_n[c->last_slot] != n) return OVH_ERR_ARG;
+  enqueue_bisect(c, c->stream, c->last_slot, (uint32_t)n, d_codes, nullptr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
 
-int ovh_combine_partials_device_async(ovh_ctx* c, size_t k, const uint8_t* d_partials, size_t n, int32_t* d_codes) {
-  if (!c || !d_partials || k == 0 || k > 16 || (n && !d_codes)) return OVH_ERR_ARG;
+int ovh_combine_partials_device_async(ovh_ctx* c, size_t k, const uint8_t* d_partials, size_t n, int32_t* d_codes,
+                                      void* stream) {
+  if (!c || !c->sub.empty() || !d_partials || k == 0 || k > 16 || (n && !d_codes)) return OVH_ERR_ARG;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  if (n != c->last_n) return OVH_ERR_ARG;
+  if (n != c->last_n || (n && c->slot_n[c->last_slot] != n)) return OVH_ERR_ARG;
   const int slot = c->last_slot;
-  // the partials were produced (and gathered) before this call returned to the host
+  hipStream_t st = (hipStream_t)stream;
+  if (st) {  // the partials are complete in `st` order (after the caller's all-gather)
+    HIPCHK(hipEventRecord(c->ev_x[2], st));
+    HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_x[2], 0));
+  }
   uint32_t* scratch = c->fin + (size_t)slot * FIN_STRIDE;
   Slab F, S;
   uint32_t m;
-  if (stage_partials(c, c->fstream, k, d_partials, scratch, &F, &S, &m)) return OVH_ERR_DEVICE;
+  CHK(stage_partials(c, c->fstream, k, d_partials, scratch, &F, &S, &m));
+  if (st) {  // the caller may reuse d_partials once they were read
+    HIPCHK(hipEventRecord(c->ev_x[3], c->fstream));
+    HIPCHK(hipStreamWaitEvent(st, c->ev_x[3], 0));
+  }
   int32_t* verdict = c->result + RES_COMBINE + slot;
   enqueue_final(c, c->fstream, F, S, m, verdict);
-  if (n) enqueue_fallback(c, c->fstream, slot, (uint32_t)n, d_codes, verdict);
+  if (n) enqueue_bisect(c, c->fstream, slot, (uint32_t)n, d_codes, verdict);
   HIPCHK(hipEventRecord(c->ev_back[slot], c->fstream));
   HIPCHK(hipGetLastError());
-  return 0;
-}
-
-int ovh_verify_batch_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
-                                  const uint8_t* d_pks, uint64_t seed, int32_t* d_codes) {
-  if (!c || (n && (!d_sigs || !d_hashes || !d_pks || !d_codes))) return OVH_ERR_ARG;
-  if (n == 0) return 0;
-  std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
-  if (ensure_cap(c, n)) return OVH_ERR_DEVICE;
-  const int slot = (int)(c->pipe_k++ % OVH_BATCH_SLOTS);
-  if (take_slot(c, slot)) return OVH_ERR_DEVICE;
-  Slab F, S;
-  uint32_t m;
-  int e = batch_front(c, (uint32_t)n, d_sigs, d_hashes, d_pks, seed, d_codes, &F, &S, &m, slot);
-  if (e) return e;
-  // fold levels: the wide ones on the main stream (short, high priority), the narrow ones and
-  // the combined check + fallback on the final stream -- balancing the two streams' chains
-  int flip = 1;
-  if ((e = fold_levels(c, c->stream, VM_SLICES, &F, &S, &m, 64, &flip))) return e;
-  HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
-  HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_front[slot], 0));
-  if ((e = fold_levels(c, c->fstream, 1, &F, &S, &m, 4, &flip))) return e;
-  int32_t* verdict = c->result + RES_BATCH + slot;
-  enqueue_final(c, c->fstream, F, S, m, verdict);
-  enqueue_fallback(c, c->fstream, slot, (uint32_t)n, d_codes, verdict);
-  HIPCHK(hipEventRecord(c->ev_back[slot], c->fstream));
-  HIPCHK(hipGetLastError());
-  return 0;
-}
-
-int ovh_batch_wait(ovh_ctx* c) {
-  if (!c) return OVH_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  HIPCHK(hipStreamSynchronize(c->fstream));
-  HIPCHK(hipStreamSynchronize(c->hstream));
-  return 0;
-}
-
-int ovh_verify_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,
-                            uint64_t seed, int32_t* d_codes) {
-  int e = ovh_verify_batch_device_async(c, n, d_sigs, d_hashes, d_pks, seed, d_codes);
-  return e ? e : ovh_batch_wait(c);
-}
-
-int ovh_verify_batch(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks, uint64_t seed,
-                     int32_t* codes) {
-  if (!c || (n && (!sigs || !hashes || !pks || !codes))) return OVH_ERR_ARG;
-  if (n == 0) return 0;
-  if (n > (1u << 24)) return OVH_ERR_ARG;
-  uint8_t* d = nullptr;
-  {
-    std::lock_guard<std::mutex> g(c->mu);
-    HIPCHK(hipSetDevice(c->device));
-    if (ensure_in(c, n * (96 + 32 + 48 + 4))) return OVH_ERR_DEVICE;
-    d = c->in_buf;
-    HIPCHK(hipMemcpyAsync(d, sigs, n * 96, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(d + n * 96, hashes, n * 32, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(d + n * 128, pks, n * 48, hipMemcpyHostToDevice, c->stream));
-  }
-  int32_t* dc = (int32_t*)(d + n * 176);
-  int e = ovh_verify_batch_device(c, n, d, d + n * 96, d + n * 128, seed, dc);
-  if (e) return e;
-  std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipMemcpyAsync(codes, dc, 4 * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }
 
 int ovh_sign_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sks, const uint8_t* d_hashes, uint8_t* d_sigs) {
-  if (!c || (n && (!d_sks || !d_hashes || !d_sigs))) return OVH_ERR_ARG;
+  if (!c || !c->sub.empty() || (n && (!d_sks || !d_hashes || !d_sigs))) return OVH_ERR_ARG;
   if (n == 0) return 0;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
@@ -1330,7 +2070,7 @@ int ovh_sign_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sks, const uint
 }
 
 int ovh_sk_to_pk_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sks, uint8_t* d_pks) {
-  if (!c || (n && (!d_sks || !d_pks))) return OVH_ERR_ARG;
+  if (!c || !c->sub.empty() || (n && (!d_sks || !d_pks))) return OVH_ERR_ARG;
   if (n == 0) return 0;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));

@@ -6,8 +6,16 @@ CPU. Every rank then runs the same combined check on the gathered partials and, 
 fails, the per-vote fallback of its own shard, so each rank ends with the exact per-vote codes
 of its votes (ConsensusCrypto::verify_signature, src/consensus.rs:397-416, vote by vote).
 
-Batches are pipelined: batch s's combined check / fallback is enqueued on the backend's second
+Batches are pipelined: batch s's combined check / bisection is enqueued on the backend's second
 stream and overlaps batch s + 1's per-vote stages; `wait()` completes everything submitted.
+The device backend is stream-ordered with torch's current stream (the stream the RCCL
+all-gather is ordered on): the partial is written after the stream's earlier work (the previous
+gather out of the same buffer) and the stream waits for it; the combined check starts after the
+gather and the stream waits until the gathered partials were read (include/ovhip.h).
+
+RLC coefficients: every rank's library context draws its own secret seed per batch (getrandom),
+so the coefficients of different ranks are independent; a backend with explicit test seeds uses
+one global vote index (index_base = the rank's shard offset), never a per-rank seed variant.
 
 The backend supplies the compute (DeviceBackend = libovhip on this rank's GPU; the CPU tests
 plug in the C oracle); this module is the orchestration both share.
@@ -32,11 +40,11 @@ class DeviceBackend:
     def empty_partials(self, world: int) -> torch.Tensor:
         return torch.empty((BATCH_SLOTS, world, PARTIAL_BYTES), dtype=torch.uint8, device="cuda")
 
-    def partial(self, sigs, hashes, pks, seed: int, codes, out_row) -> None:
-        self.dev.batch_partial(self.ctx, sigs, hashes, pks, seed, codes, out_row)
+    def partial(self, sigs, hashes, pks, codes, out_row, index_base: int) -> None:
+        self.dev.batch_partial(self.ctx, sigs, hashes, pks, codes, out_row, stream=True)
 
     def combine_async(self, parts, n: int, codes) -> None:
-        self.dev.combine_partials_async(self.ctx, parts, n, codes)
+        self.dev.combine_partials_async(self.ctx, parts, n, codes, stream=True)
 
     def wait(self) -> None:
         self.dev.batch_wait(self.ctx)
@@ -60,12 +68,12 @@ class ShardVerifier:
         else:
             dist.all_gather(list(part.unbind(0)), mine, group=self.group)
 
-    def submit(self, s: int, sigs, hashes, pks, seed: int, codes) -> None:
-        """Enqueue batch s: this rank's n votes -> partial -> all-gather -> combined check and
-        (device-gated) fallback into `codes`, final after wait()."""
+    def submit(self, s: int, sigs, hashes, pks, codes, index_base: int = 0) -> None:
+        """Enqueue batch s: this rank's n votes (global indices index_base ..) -> partial ->
+        all-gather -> combined check and (device-gated) bisection into `codes`, final after
+        wait()."""
         part = self.partials[s % self.partials.shape[0]]
-        seed = (seed ^ (self.rank * 0x9E3779B97F4A7C15)) & 0xFFFFFFFFFFFFFFFF   # rank-distinct RLC scalars
-        self.backend.partial(sigs, hashes, pks, seed, codes, part[self.rank])
+        self.backend.partial(sigs, hashes, pks, codes, part[self.rank], index_base)
         self._all_gather(part)
         self.backend.combine_async(part, sigs.shape[0], codes)
 

@@ -1,8 +1,11 @@
 /*
  * libovhip — MI355X (gfx950) BLS12-381 signature backend for the overlord `Crypto` trait of
  * cita-cloud/consensus_overlord. C ABI: plain pointers and sizes, caller-owned host buffers,
- * no pointer is retained after a call returns. All arithmetic runs in HIP kernels; there is
- * no CPU fallback (a missing/failed device returns OVH_ERR_DEVICE).
+ * no pointer is retained after a call returns. All curve arithmetic runs in HIP kernels; there
+ * is no CPU fallback (a missing/failed device returns OVH_ERR_DEVICE). Every entry point is
+ * thread-safe: a context serialises its device work internally (the trait object is Send +
+ * Sync and is called concurrently by overlord and the gRPC check_block handler,
+ * src/main.rs:107-127 -> src/consensus.rs:176).
  *
  * Return codes (int):
  *   0        OK
@@ -13,8 +16,9 @@
  *   101      len(signatures) != len(voters)
  *                                     -> Other("signatures length does not match voters length")
  *   102      a public key does not parse -> Other("lose public key")
- *   103      invalid argument (NULL pointer, n too large)
+ *   103      invalid argument (NULL pointer, n too large, wrong context kind)
  *   200      HIP device error
+ *   201      the OS random source (getrandom) failed
  *
  * Variable-length lists (Rust `Vec<Bytes>`) are passed as one concatenated byte buffer plus
  * an array of item lengths.
@@ -37,34 +41,53 @@ typedef struct ovh_ctx ovh_ctx;
 #define OVH_ERR_PUBKEY 102
 #define OVH_ERR_ARG 103
 #define OVH_ERR_DEVICE 200
+#define OVH_ERR_RNG 201
 
-/* Flags for ovh_create. */
+/* Flags for ovh_create / ovh_create_multi. */
 #define OVH_FLAG_AGG_NO_GROUPCHECK 0x1u /* aggregate_signatures without the G2 subgroup check */
 #define OVH_FLAG_PROFILE 0x2u           /* record HIP events around every batch stage */
 #define OVH_FLAG_VM_TRACE 0x4u          /* diagnostics: per-phase clock of the VM kernels' workgroup 0 */
+#define OVH_FLAG_TEST_RLC 0x8u          /* TESTS ONLY: batch coefficients from ovh_set_test_rlc (predictable) */
+#define OVH_FLAG_SK_RAW 0x10u           /* private key = 32-byte big-endian scalar 0 < sk < r (blst
+                                           SecretKey::from_bytes) instead of KeyGen (see ovh_sk_parse) */
 
-/* Batch stages (ovh_stage_name gives the label). Each stage is one or more kernels enqueued
- * back to back on ovh_stream. */
+/* Batch stages (ovh_stage_name gives the label). Each stage is one or more kernels. */
 #define OVH_NSTAGES 5
 
 /* Create a context on HIP device `device` with hash-to-curve domain separation tag `dst`
  * (NULL -> "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_", the believed ophelia-blst DST).
  * Replaces ConsensusCrypto::new's crypto state (src/consensus.rs:347-359). NULL on failure. */
 ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t flags);
+/* One context over several GPUs of this process: ovh_verify_batch and
+ * ovh_prefetch split a batch into contiguous shards, one per device; each device computes its
+ * shard's 864-byte partial, the partials are copied peer-to-peer (xGMI) to devices[0], which
+ * runs the one combined check; on failure every device bisects its own shard. Single-call
+ * entry points rotate over the devices. Devices may repeat (tests use {0, 0}). */
+ovh_ctx* ovh_create_multi(const int* devices, int ndev, const uint8_t* dst, size_t dst_len, uint32_t flags);
 void ovh_destroy(ovh_ctx* ctx);
-/* The HIP stream (hipStream_t) all of the context's kernels run on. */
+/* Number of devices of the context (1 for ovh_create). */
+int ovh_device_count(ovh_ctx* ctx);
+/* The HIP stream (hipStream_t) the context's per-vote kernels run on (first device). */
 void* ovh_stream(ovh_ctx* ctx);
 
 /* Crypto::hash -> util.rs:83-87 sm3_hash. */
 int ovh_sm3(const uint8_t* msg, size_t len, uint8_t out[32]);
 
-/* Crypto::sign (consensus.rs:390-395): sigma = sk * H(hash), 96-byte compressed.
- * sk: 32-byte big-endian scalar, 0 < sk < r (else BLST_BAD_ENCODING). */
-int ovh_sign(ovh_ctx* ctx, const uint8_t* sk, size_t sk_len, const uint8_t* hash, size_t hash_len, uint8_t out[96]);
-/* BlsPrivateKey::pub_key + to_bytes (consensus.rs:352,357): 48-byte compressed pk. */
-int ovh_sk_to_pk(ovh_ctx* ctx, const uint8_t* sk, size_t sk_len, uint8_t out[48]);
+/* BlsPrivateKey::try_from (consensus.rs:349-350, ophelia-blst [dep]): the 32-byte scalar the
+ * context signs with, big-endian. Default: IETF KeyGen (blst SecretKey::key_gen(key, ""):
+ * HKDF-SHA256, key >= 32 bytes) -- the reference's own example/private_key is >= r, so the
+ * parse cannot be blst's strict from_bytes. With OVH_FLAG_SK_RAW: 32 bytes, 0 < sk < r.
+ * BLST_BAD_ENCODING (1) when the key does not parse. Host only (no device work). */
+int ovh_sk_parse(ovh_ctx* ctx, const uint8_t* key, size_t key_len, uint8_t out_scalar[32]);
 
-/* Crypto::verify_signature (consensus.rs:397-416). */
+/* Crypto::sign (consensus.rs:390-395): sigma = sk * H(hash), 96-byte compressed; `key` is the
+ * private key bytes as ConsensusCrypto::new reads them (ovh_sk_parse). */
+int ovh_sign(ovh_ctx* ctx, const uint8_t* key, size_t key_len, const uint8_t* hash, size_t hash_len, uint8_t out[96]);
+/* BlsPrivateKey::pub_key + to_bytes (consensus.rs:352,357): 48-byte compressed pk. */
+int ovh_sk_to_pk(ovh_ctx* ctx, const uint8_t* key, size_t key_len, uint8_t out[48]);
+
+/* Crypto::verify_signature (consensus.rs:397-416). Answers from the verdict cache when the
+ * (sig, hash, voter) triple was batch-verified by ovh_prefetch; otherwise one device check. */
 int ovh_verify(ovh_ctx* ctx, const uint8_t* sig, size_t sig_len, const uint8_t* hash, size_t hash_len,
                const uint8_t* pk, size_t pk_len);
 
@@ -79,65 +102,102 @@ int ovh_aggregate_pks(ovh_ctx* ctx, const uint8_t* pks, const size_t* pk_lens, s
 int ovh_verify_aggregated(ovh_ctx* ctx, const uint8_t* agg_sig, size_t agg_len, const uint8_t* hash, size_t hash_len,
                           const uint8_t* pks, const size_t* pk_lens, size_t n);
 
+/* ConsensusCrypto::update_pubkeys (consensus.rs:361-363; callers proc_reconfigure :131-136 and
+ * Brain::commit :622-629): n x 48-byte compressed validator keys, in the order the node's config
+ * lists them. Each key is decompressed and group-checked once on the device and kept as a
+ * point in HBM. ovh_verify_batch / ovh_prefetch then skip the per-vote key decompression for
+ * voters found in the table, and ovh_verify_qc_batch selects QC voters from it. Keys that do
+ * not parse are kept (their votes answer 102, as the reference's per-call parse would). */
+int ovh_set_validators(ovh_ctx* ctx, const uint8_t* pks, size_t n);
+
 /* Batched verify_signature over n votes (fixed-size compressed encodings):
- * sigs n x 96 B, hashes n x 32 B, pks n x 48 B -> codes[n] with exactly the per-vote
- * ovh_verify result. Random-linear-combination check (64-bit scalars from `seed`) with a
- * per-vote fallback when the combined check fails. Returns 0 if the batch ran (the verdicts
- * are in codes), else an error. Host buffers. */
+ * sigs n x 96 B, hashes n x 32 B, pks n x 48 B -> codes[n], codes[i] == the ovh_verify result
+ * for vote i. One random-linear-combination check with secret 64-bit coefficients (a fresh
+ * getrandom seed per batch) and, when it fails, a bisection: 16-vote groups, then per-vote
+ * checks in the failing groups on the device-resident Miller outputs. Host buffers. */
 int ovh_verify_batch(ovh_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
-                     uint64_t seed, int32_t* codes);
+                     int32_t* codes);
 
-/* The same with device-resident inputs/outputs (pointers into HBM), enqueued on ovh_stream;
- * the call returns after the batch completed. */
+/* Vote-batching ingress: batch-verify n votes as they arrive at
+ * proc_network_msg (consensus.rs:210-262) and keep each verdict in the context's cache, keyed
+ * by the exact (sig, hash, voter) bytes; overlord's later serial verify_signature calls
+ * (ovh_verify) are then answered from the cache. Bounded FIFO cache (ovh_cache_config). */
+int ovh_prefetch(ovh_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks);
+/* Cache capacity in entries (0 disables the cache and empties it). Default 65536. */
+int ovh_cache_config(ovh_ctx* ctx, size_t capacity);
+/* stats[0] = hits, stats[1] = misses (fixed-size triples not in the cache), stats[2] = entries. */
+int ovh_cache_stats(ovh_ctx* ctx, uint64_t stats[3]);
+
+/* Batched QC verification for block sync (check_block, consensus.rs:143-207): QC j = aggregated
+ * signature sigs[j] (96 B) over hashes[j] (32 B, the SM3 of rlp(Vote{h, r, Precommit, block})),
+ * signed by the validators whose bits are set in bitmaps[j] (bitmap_len bytes, MSB first) over
+ * the validator table sorted by key bytes (overlord extract_voters over the address-sorted
+ * authority list; validators_to_nodes uses the key bytes as the address, util.rs:69-77).
+ * codes[j] == ovh_verify_aggregated(sigs[j], hashes[j], those voters). One RLC batch over all
+ * QCs. Needs ovh_set_validators. */
+int ovh_verify_qc_batch(ovh_ctx* ctx, size_t nq, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* bitmaps,
+                        size_t bitmap_len, int32_t* codes);
+
+/* TESTS ONLY (context created with OVH_FLAG_TEST_RLC, else OVH_ERR_ARG): vote i of every
+ * following batch gets the coefficient SplitMix64(seed, index_base + i). Predictable
+ * coefficients let an adversary cancel invalid signatures inside the combined check
+ * (tests/test_rlc_soundness.py); production contexts never use this. */
+int ovh_set_test_rlc(ovh_ctx* ctx, uint64_t seed, uint64_t index_base);
+
+/* The same as ovh_verify_batch with device-resident inputs/outputs (pointers into HBM), enqueued
+ * on the context's streams; returns after the batch completed. */
 int ovh_verify_batch_device(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
-                            const uint8_t* d_pks, uint64_t seed, int32_t* d_codes);
+                            const uint8_t* d_pks, int32_t* d_codes);
 
-/* Multi-GPU split of ovh_verify_batch_device: per-shard partial = {Fp12 product of the
- * shard's Miller outputs (576 B), projective G2 sum of r_i sigma_i (288 B)} = 864 bytes,
- * written to d_partial (device memory). Per-vote parse/subgroup codes go to d_codes.
- * The G2 sum is in homogeneous projective coordinates (X : Y : Z), O = (0 : 1 : 0). */
+/* Multi-GPU split of ovh_verify_batch_device (one process per GPU): per-shard partial =
+ * {Fp12 product of the shard's Miller outputs (576 B), projective G2 sum of r_i sigma_i
+ * (288 B)} = 864 bytes, written to d_partial (device memory); per-vote parse/subgroup codes go
+ * to d_codes. The G2 sum is in homogeneous projective coordinates (X : Y : Z), O = (0 : 1 : 0).
+ * Stream order: `stream` (a hipStream_t of the caller, e.g. torch's current stream) -- the
+ * partial is written after the work already on `stream` (so a gather buffer can be reused) and
+ * `stream` waits for the write; the call returns without blocking. stream NULL: the call
+ * returns once d_partial is written. */
 #define OVH_PARTIAL_BYTES 864
 int ovh_batch_partial_device(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
-                             const uint8_t* d_pks, uint64_t seed, int32_t* d_codes, uint8_t* d_partial);
-/* Combine k partials (device memory, k x 864 B): returns 1 if prod f * e(-G1, sum S) == 1
- * after the final exponentiation, 0 if not, <0 on device error. */
-int ovh_combine_partials_device(ovh_ctx* ctx, size_t k, const uint8_t* d_partials);
-/* Per-vote fallback for a shard whose combined check failed: codes[i] (device) updated to the
- * exact per-vote verify result for every vote whose code is still 0. */
+                             const uint8_t* d_pks, int32_t* d_codes, uint8_t* d_partial, void* stream);
+/* Combine k partials (device memory, k x 864 B): *verdict = 1 if prod f * e(-G1, sum S) == 1
+ * after the final exponentiation, else 0. Synchronous; returns 0 or an error code. */
+int ovh_combine_partials_device(ovh_ctx* ctx, size_t k, const uint8_t* d_partials, int32_t* verdict);
+/* Bisection of the last ovh_batch_partial_device shard (its combined check failed): d_codes[i]
+ * still 0 -> the exact per-vote verify result. Synchronous. */
 int ovh_batch_fallback_device(ovh_ctx* ctx, size_t n, int32_t* d_codes);
 
 /* Pipelined batches. ovh_verify_batch_device_async enqueues one batch and returns without
- * waiting: the per-vote stages run on ovh_stream, the combined check and (device-gated) per-vote
- * fallback on a second, lower-priority stream, so batch k's final exponentiation overlaps batch
+ * waiting: the per-vote stages run on ovh_stream, the combined check and (device-gated)
+ * bisection on a second, lower-priority stream, so batch k's final exponentiation overlaps batch
  * k + 1's per-vote work. Up to OVH_BATCH_SLOTS batches may be in flight per context; the
  * d_codes of a batch must stay untouched until ovh_batch_wait returns, after which they hold
- * exactly the per-vote ovh_verify results. ovh_verify_batch_device = the async call +
- * ovh_batch_wait. */
+ * exactly the per-vote ovh_verify results. */
 #define OVH_BATCH_SLOTS 2 /* batches in flight per context (state slots) */
 int ovh_verify_batch_device_async(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
-                                  const uint8_t* d_pks, uint64_t seed, int32_t* d_codes);
+                                  const uint8_t* d_pks, int32_t* d_codes);
 int ovh_batch_wait(ovh_ctx* ctx);
 /* Multi-GPU form: after ovh_batch_partial_device (n votes of this rank) and the all-gather of
- * the k <= 16 partials, enqueue the combined check and, if it fails, the per-vote fallback of
- * this rank's n votes into d_codes, on the second stream; ovh_batch_wait completes it. */
+ * the k <= 16 partials on `stream`, enqueue (stream-ordered after the gather) the combined check
+ * and, if it fails, the bisection of this rank's n votes into d_codes; `stream` waits until the
+ * partials were read. ovh_batch_wait completes it. */
 int ovh_combine_partials_device_async(ovh_ctx* ctx, size_t k, const uint8_t* d_partials, size_t n,
-                                      int32_t* d_codes);
+                                      int32_t* d_codes, void* stream);
 
-/* Device time (ms, HIP events on ovh_stream) of each stage of the most recent batch call
- * (ovh_verify_batch_device / ovh_batch_partial_device / ovh_combine_partials_device /
- * ovh_batch_fallback_device) on a context created with OVH_FLAG_PROFILE; stages that did not
- * run read 0. Fills min(max, OVH_NSTAGES) entries and returns that count (0 without the
- * flag, <0 on error). */
+/* Device time (ms, HIP events) of each stage of the most recent batch call on a context created
+ * with OVH_FLAG_PROFILE; stages that did not run read 0. Fills min(max, OVH_NSTAGES) entries
+ * and returns that count (0 without the flag, <0 on error). */
 int ovh_stage_times(ovh_ctx* ctx, float* ms, size_t max);
 const char* ovh_stage_name(int stage);
 
-/* Diagnostics (context created with OVH_FLAG_VM_TRACE): the wall clock (100 MHz counter)
- * workgroup 0 of the last launch of VM program `prog` (0 vote, 1 fold, 2 final, 3 pairchk)
+/* Diagnostics (context created with OVH_FLAG_VM_TRACE): the wall clock (100 MHz counter) of
+ * workgroup 0 of the last launch of VM program `prog` (0 vote, 1 fold, 2 final, 3 vote_t)
  * read after each phase barrier: copies min(max, nphases + 1) stamps, returns nphases + 1
  * (0 without the flag, <0 on error). */
 int ovh_vm_trace(ovh_ctx* ctx, int prog, uint64_t* stamps, size_t max);
 
-/* Batched helpers used to synthesise workloads on the device. */
+/* Batched helpers used to synthesise workloads on the device; d_sks are 32-byte big-endian
+ * scalars (not key files). */
 int ovh_sign_batch_device(ovh_ctx* ctx, size_t n, const uint8_t* d_sks, const uint8_t* d_hashes, uint8_t* d_sigs);
 int ovh_sk_to_pk_batch_device(ovh_ctx* ctx, size_t n, const uint8_t* d_sks, uint8_t* d_pks);
 

@@ -12,6 +12,7 @@
  *   orc_aggregate_pks       BlsPublicKey::aggregate                 consensus.rs:371
  *   orc_verify_aggregated   verify_aggregated_signature + inner_... consensus.rs:446-462, 365-382
  *   orc_sign / orc_sk_to_pk ConsensusCrypto::sign / new             consensus.rs:390-395, 347-359
+ *   orc_sk_keygen           BlsPrivateKey::try_from = IETF KeyGen  consensus.rs:349-350 (see below)
  *   orc_verify_many         the serial per-vote shape overlord drives, threaded
  *   orc_verify_batch_rlc    the random-linear-combination batch check the GPU runs, threaded
  *
@@ -1255,6 +1256,86 @@ static int sk_parse(uint64_t k[4], const uint8_t* sk, size_t len) {
   return OK;
 }
 
+/* ophelia-blst BlsPrivateKey::try_from (consensus.rs:349-350) [dep]: blst SecretKey::key_gen(ikm,
+ * "") = IETF KeyGen (draft-irtf-cfrg-bls-signature-04 2.3; = EIP-2333 HKDF_mod_r): salt =
+ * SHA-256("BLS-SIG-KEYGEN-SALT-"); PRK = HKDF-Extract(salt, IKM || 0x00); OKM = HKDF-Expand(PRK,
+ * 0x0030, 48); SK = OS2IP(OKM) mod r, re-hashing the salt while SK = 0. ikm >= 32 bytes. */
+static void hmac_sha256(uint8_t out[32], const uint8_t* key, size_t klen, const uint8_t* msg, size_t mlen) {
+  uint8_t k[64], buf[64 + 256], inner[32];
+  memset(k, 0, sizeof k);
+  if (klen > 64) sha256(k, key, klen);
+  else memcpy(k, key, klen);
+  if (mlen > 256) return; /* callers stay below */
+  for (int i = 0; i < 64; ++i) buf[i] = k[i] ^ 0x36;
+  memcpy(buf + 64, msg, mlen);
+  sha256(inner, buf, 64 + mlen);
+  for (int i = 0; i < 64; ++i) buf[i] = k[i] ^ 0x5c;
+  memcpy(buf + 64, inner, 32);
+  sha256(out, buf, 96);
+}
+
+static const uint8_t R_ORDER_BE[32] = {0x73, 0xed, 0xa7, 0x53, 0x29, 0x9d, 0x7d, 0x48, 0x33, 0x39, 0xd8,
+                                       0x08, 0x09, 0xa1, 0xd8, 0x05, 0x53, 0xbd, 0xa4, 0x02, 0xff, 0xfe,
+                                       0x5b, 0xfe, 0xff, 0xff, 0xff, 0xff, 0x00, 0x00, 0x00, 0x01};
+
+/* out = OS2IP(in[0..48)) mod r: 384-bit value as 6 limbs, reduced by 128-bit arithmetic on the
+ * 4-limb order with shift-and-subtract over the bits */
+static void os2ip_mod_r(uint8_t out[32], const uint8_t in[48]) {
+  uint64_t r[4], a[5] = {0, 0, 0, 0, 0};
+  for (int i = 0; i < 4; ++i) {
+    uint64_t x = 0;
+    for (int b = 0; b < 8; ++b) x = (x << 8) | R_ORDER_BE[24 - 8 * i + b];
+    r[i] = x;
+  }
+  for (int bit = 0; bit < 384; ++bit) {
+    const uint64_t in_bit = (in[bit / 8] >> (7 - bit % 8)) & 1;
+    for (int i = 4; i > 0; --i) a[i] = (a[i] << 1) | (a[i - 1] >> 63);
+    a[0] = (a[0] << 1) | in_bit;
+    int ge = a[4] != 0;
+    if (!ge) {
+      ge = 1;
+      for (int i = 3; i >= 0; --i)
+        if (a[i] != r[i]) {
+          ge = a[i] > r[i];
+          break;
+        }
+    }
+    if (ge) {
+      uint64_t br = 0;
+      for (int i = 0; i < 4; ++i) {
+        u128 d = (u128)a[i] - r[i] - br;
+        a[i] = (uint64_t)d;
+        br = (uint64_t)(d >> 64) & 1;
+      }
+      a[4] -= br;
+    }
+  }
+  for (int i = 0; i < 4; ++i)
+    for (int b = 0; b < 8; ++b) out[24 - 8 * i + b] = (uint8_t)(a[i] >> (56 - 8 * b));
+}
+
+int orc_sk_keygen(const uint8_t* ikm, size_t len, uint8_t out32[32]) {
+  if (!ikm || len < 32 || len > 200 || !out32) return BAD_ENCODING;
+  uint8_t salt[32], prk[32], okm[64], msg[256];
+  sha256(salt, (const uint8_t*)"BLS-SIG-KEYGEN-SALT-", 20);
+  for (;;) {
+    memcpy(msg, ikm, len);
+    msg[len] = 0; /* IKM || I2OSP(0, 1) */
+    hmac_sha256(prk, salt, 32, msg, len + 1);
+    /* T(1) = HMAC(PRK, info || 1), T(2) = HMAC(PRK, T(1) || info || 2); info = I2OSP(48, 2) */
+    uint8_t m1[3] = {0x00, 0x30, 0x01}, m2[35];
+    hmac_sha256(okm, prk, 32, m1, 3);
+    memcpy(m2, okm, 32);
+    m2[32] = 0x00;
+    m2[33] = 0x30;
+    m2[34] = 0x02;
+    hmac_sha256(okm + 32, prk, 32, m2, 35);
+    os2ip_mod_r(out32, okm);
+    if (!all_zero(out32, 32)) return OK;
+    sha256(salt, salt, 32);
+  }
+}
+
 int orc_sk_to_pk(const uint8_t* sk, size_t sk_len, uint8_t out48[48]) {
   init();
   uint64_t k[4];
@@ -1414,7 +1495,7 @@ typedef struct {
   size_t lo, hi;
   const uint8_t *sigs, *hashes, *pks;
   int32_t* codes;
-  uint64_t seed;
+  uint64_t seed, base; /* vote i's coefficient: SplitMix64(seed, base + i) */
   fp12 f;
   g2_jac S;
 } job_t;
@@ -1528,7 +1609,7 @@ static void* rlc_worker(void* arg) {
     /* r = a + b lambda (mod r), lambda = -x^2, (a, b) = the 32-bit halves of SplitMix64 (the
      * device's tools/fpvm/alg.py LAMBDA): [r] pk = [a] pk + [b] phi(pk), [r] sig = [a] sig +
      * [b] (-psi^2(sig)); pk in G1 and sig in G2 were checked above. */
-    const uint64_t r = splitmix(j->seed, i);
+    const uint64_t r = splitmix(j->seed, j->base + i);
     const uint32_t ra = (uint32_t)r, rb = (uint32_t)(r >> 32);
     g1_jac rp, phi = pj;
     fp_mul(&phi.X, &pj.X, &BETA);
@@ -1630,7 +1711,7 @@ static void part_read(fp12* f, g2_jac* S, const uint8_t* in) {
 /* Per-shard partial of the RLC batch (codes[i] = parse / subgroup codes, OK for the votes
  * that entered the partial); out864 as above. */
 int orc_batch_partial(size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks, uint64_t seed,
-                      int32_t* codes, int threads, uint8_t* out864) {
+                      uint64_t base, int32_t* codes, int threads, uint8_t* out864) {
   init();
   if (threads < 1) threads = 1;
   fp12 f;
@@ -1640,6 +1721,7 @@ int orc_batch_partial(size_t n, const uint8_t* sigs, const uint8_t* hashes, cons
   if (n) {
     job_t* jobs = make_jobs(n, threads, sigs, hashes, pks, codes, seed);
     if (!jobs) return ERR_ARG;
+    for (int t = 0; t < threads; ++t) jobs[t].base = base;
     run_jobs(jobs, threads, rlc_worker);
     for (int t = 0; t < threads; ++t) {
       f12_mul(&f, &f, &jobs[t].f);

@@ -27,6 +27,7 @@ psi-endomorphism formula, and pairing bilinearity.
 from __future__ import annotations
 
 import hashlib
+import hmac
 
 # ----------------------------------------------------------------------------------------
 # Parameters
@@ -858,8 +859,41 @@ def multi_pairing_is_one(pairs) -> bool:
 # ----------------------------------------------------------------------------------------
 
 
+def hkdf_extract(salt: bytes, ikm: bytes) -> bytes:
+    """RFC 5869 HKDF-Extract with SHA-256."""
+    return hmac.new(salt, ikm, hashlib.sha256).digest()
+
+
+def hkdf_expand(prk: bytes, info: bytes, length: int) -> bytes:
+    """RFC 5869 HKDF-Expand with SHA-256."""
+    t, okm, i = b"", b"", 1
+    while len(okm) < length:
+        t = hmac.new(prk, t + info + bytes([i]), hashlib.sha256).digest()
+        okm += t
+        i += 1
+    return okm[:length]
+
+
+def sk_keygen(ikm: bytes, key_info: bytes = b"") -> int:
+    """blst `SecretKey::key_gen(ikm, key_info)` = IETF KeyGen (draft-irtf-cfrg-bls-signature-04
+    section 2.3, identical to EIP-2333 HKDF_mod_r): what ophelia-blst's
+    `BlsPrivateKey::try_from` [dep] must be, since the reference parses its own
+    example/private_key (>= r) without error (src/consensus.rs:349-350)."""
+    ikm = bytes(ikm)
+    if len(ikm) < 32:
+        raise BlstError(BLST_BAD_ENCODING)
+    salt = b"BLS-SIG-KEYGEN-SALT-"
+    sk = 0
+    while sk == 0:
+        salt = hashlib.sha256(salt).digest()
+        okm = hkdf_expand(hkdf_extract(salt, ikm + b"\x00"), key_info + (48).to_bytes(2, "big"), 48)
+        sk = int.from_bytes(okm, "big") % R
+    return sk
+
+
 def sk_from_bytes(b: bytes) -> int:
-    """blst `SecretKey::from_bytes`: 32-byte big-endian scalar, 0 < sk < r."""
+    """blst `SecretKey::from_bytes` (the OVH_FLAG_SK_RAW alternative): 32-byte big-endian
+    scalar, 0 < sk < r."""
     b = bytes(b)
     if len(b) != 32:
         raise BlstError(BLST_BAD_ENCODING)

@@ -39,7 +39,9 @@ def load(build_if_missing: bool = True):
         "orc_verify_batch_rlc": (ctypes.c_int, [_sz, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int,
                                                 ctypes.POINTER(ctypes.c_int)]),
         "orc_gt_g1g2": (None, [_u8]),
-        "orc_batch_partial": (ctypes.c_int, [_sz, _vp, _vp, _vp, ctypes.c_uint64, _vp, ctypes.c_int, _vp]),
+        "orc_batch_partial": (ctypes.c_int, [_sz, _vp, _vp, _vp, ctypes.c_uint64, ctypes.c_uint64, _vp, ctypes.c_int,
+                                             _vp]),
+        "orc_sk_keygen": (ctypes.c_int, [_u8, _sz, _u8]),
         "orc_combine_partials": (ctypes.c_int, [_sz, _vp, ctypes.POINTER(ctypes.c_int)]),
         "orc_batch_fallback": (ctypes.c_int, [_sz, _vp, _vp, _vp, _vp, ctypes.c_int]),
     }
@@ -138,16 +140,25 @@ def gt_g1g2() -> list:
     return ["%096x" % int.from_bytes(out.raw[48 * i:48 * i + 48], "big") for i in range(12)]
 
 
-def batch_partial(sigs, hashes, pks, seed: int, threads: int = 1):
-    """orc_batch_partial: -> (codes, 864-byte partial in libovhip's format)."""
+def sk_keygen(ikm: bytes):
+    """orc_sk_keygen (IETF KeyGen, BlsPrivateKey::try_from): -> (code, 32-byte scalar)."""
+    out = ctypes.create_string_buffer(32)
+    c = load().orc_sk_keygen(ikm, len(ikm), out)
+    return c, (out.raw if c == 0 else None)
+
+
+def batch_partial(sigs, hashes, pks, seed: int, threads: int = 1, base: int = 0):
+    """orc_batch_partial: -> (codes, 864-byte partial in libovhip's format); vote i's
+    coefficient is SplitMix64(seed, base + i)."""
     s, sp = _arr(sigs, 96)
     h, hp = _arr(hashes, 32)
     p, pp = _arr(pks, 48)
     n = s.shape[0]
     codes = np.zeros(max(n, 1), dtype=np.int32)
     out = np.zeros(864, dtype=np.uint8)
-    assert load().orc_batch_partial(n, sp, hp, pp, seed & 0xFFFFFFFFFFFFFFFF, codes.ctypes.data_as(ctypes.c_void_p),
-                                    threads, out.ctypes.data_as(ctypes.c_void_p)) == 0
+    assert load().orc_batch_partial(n, sp, hp, pp, seed & 0xFFFFFFFFFFFFFFFF, base,
+                                    codes.ctypes.data_as(ctypes.c_void_p), threads,
+                                    out.ctypes.data_as(ctypes.c_void_p)) == 0
     return codes[:n], out
 
 

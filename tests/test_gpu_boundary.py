@@ -1,0 +1,153 @@
+"""The drop-in boundary on the GPU (include/ovhip.h): thread safety of one context, the
+vote-batching verdict cache (ovh_prefetch -> ovh_verify), the device validator table
+(ovh_set_validators -> vote_t path) and batched QC verification (ovh_verify_qc_batch), each
+checked against the oracle / golden codes."""
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import synth_votes as sv
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(os.path.join(ROOT, "tests", "golden", "golden_v1.json")) as fh:
+        return json.load(fh)
+
+
+def _fixed(golden):
+    return [c for c in golden["verify"] if len(c["sig"]) == 192 and len(c["hash"]) == 64 and len(c["pk"]) == 96]
+
+
+def _b(h):
+    return bytes.fromhex(h)
+
+
+def test_two_threads_one_context(golden):
+    """overlord's serial verify_signature and a gRPC-side batch on the same context at once
+    (main.rs:107-127): every call returns its exact codes."""
+    import consensus_overlord_amd as coa
+    c = coa.ConsensusCrypto(bytes.fromhex("55" * 32))
+    cases = _fixed(golden)
+    n = 512
+    sigs, hs, pks = sv.make(c.ctx, n, lo=90000)
+    for k, i in enumerate(range(0, n, 97)):
+        sigs[i] = np.frombuffer(sv.add_g2(bytes(sigs[i])), dtype=np.uint8)
+    want = sv.oracle_codes(sigs, hs, pks)
+    errors = []
+
+    def serial():
+        try:
+            for _ in range(2):
+                for cs in cases:
+                    got = c.lib.ovh_verify(c.ctx.ptr, _b(cs["sig"]), 96, _b(cs["hash"]), 32, _b(cs["pk"]), 48)
+                    if got != cs["code"]:
+                        errors.append(("verify", cs["name"], got))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    def batch():
+        try:
+            for _ in range(3):
+                got = c.verify_batch(list(map(bytes, sigs)), list(map(bytes, hs)), list(map(bytes, pks)))
+                if got.tolist() != want.tolist():
+                    errors.append(("batch", got))
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+    th = [threading.Thread(target=serial), threading.Thread(target=batch)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors[:3]
+
+
+def test_prefetch_then_serial_verify_hits_cache(golden):
+    import consensus_overlord_amd as coa
+    from consensus_overlord_amd.crypto import CryptoErr, Other
+    c = coa.ConsensusCrypto(bytes.fromhex("66" * 32))
+    cases = _fixed(golden)
+    sigs, hs, pks = [_b(x["sig"]) for x in cases], [_b(x["hash"]) for x in cases], [_b(x["pk"]) for x in cases]
+    c.prefetch(sigs, hs, pks)
+    h0, m0, e0 = c.cache_stats()
+    assert e0 == len(set(zip(sigs, hs, pks)))
+    for cs, s, h, p in zip(cases, sigs, hs, pks):
+        try:
+            c.verify_signature(s, h, p)
+            got = 0
+        except CryptoErr as e:
+            got = e.code
+        except Other as e:
+            got = {"lose public key": 102}[str(e)]
+        assert got == cs["code"], cs["name"]
+    h1, m1, _ = c.cache_stats()
+    assert h1 - h0 == len(cases) and m1 == m0
+    # a triple not prefetched is a miss and still exact
+    c.verify_signature(sigs[0], hs[0], pks[0])
+    assert c.lib.ovh_verify(c.ctx.ptr, sigs[1], 96, hs[0], 32, pks[0], 48) == 5
+    assert c.cache_stats()[1] == m1 + 1
+
+
+def test_validator_table_path_matches_golden(golden):
+    """update_pubkeys with every fixed-size golden key (including keys that do not parse, the
+    infinity key and a non-G1 key): verify_batch then runs the table (vote_t) path."""
+    import consensus_overlord_amd as coa
+    c = coa.ConsensusCrypto(bytes.fromhex("77" * 32))
+    cases = _fixed(golden)
+    keys = sorted(set(_b(x["pk"]) for x in cases))
+    c.update_pubkeys(keys)
+    got = c.verify_batch([_b(x["sig"]) for x in cases], [_b(x["hash"]) for x in cases], [_b(x["pk"]) for x in cases])
+    for cs, g in zip(cases, got):
+        assert g == cs["code"], cs["name"]
+    # per call through the table too
+    for cs in cases[:12]:
+        assert c.lib.ovh_verify(c.ctx.ptr, _b(cs["sig"]), 96, _b(cs["hash"]), 32, _b(cs["pk"]), 48) == cs["code"]
+
+
+def _bitmap(sorted_keys, voters, nbytes):
+    bm = bytearray(nbytes)
+    pos = {k: i for i, k in enumerate(sorted_keys)}
+    for v in voters:
+        i = pos[v]
+        bm[i // 8] |= 0x80 >> (i % 8)
+    return bytes(bm)
+
+
+def test_qc_batch_matches_verify_aggregated(golden):
+    """check_block's QC check (consensus.rs:143-207) batched over QCs: voters from the bitmap
+    over the key-sorted validator table (extract_voters)."""
+    import consensus_overlord_amd as coa
+    import orc
+    c = coa.ConsensusCrypto(bytes.fromhex("88" * 32))
+    q = golden["qc"]
+    pks = [_b(p) for p in q["pks"]]
+    bad_parse = _b([x for x in golden["verify"] if x["name"] == "pk_x_eq_p"][0]["pk"])
+    not_g1 = _b([x for x in golden["verify"] if x["name"] == "pk_not_in_g1"][0]["pk"])
+    table = pks + [bad_parse, not_g1]
+    c.update_pubkeys(table)
+    skeys = sorted(table)
+    nb = (len(table) + 7) // 8
+    agg, h = _b(q["agg_sig"]), _b(q["hash"])
+    qcs = [
+        (agg, h, pks[:67]),                 # valid QC (config 2)
+        (agg, h, pks[:66]),                 # one signer missing
+        (agg, bytes(32), pks[:67]),         # wrong vote hash
+        (agg, h, []),                       # empty bitmap -> AGGR_TYPE_MISMATCH
+        (agg, h, pks[:67] + [bad_parse]),   # a voter key that does not parse -> 102
+        (agg, h, pks[:66] + [not_g1]),      # a voter key outside G1 (exact single-QC path)
+        (_b(q["sigs"][0]), h, [pks[0]]),    # single-signer QC
+    ]
+    sigs = [x[0] for x in qcs]
+    hashes = [x[1] for x in qcs]
+    bitmaps = [_bitmap(skeys, x[2], nb) for x in qcs]
+    got = c.verify_qc_batch(sigs, hashes, bitmaps)
+    want = [orc.verify_aggregated(s, hh, list(v)) for s, hh, v in qcs]
+    assert got.tolist() == want
+    assert want[:4] == [0, 5, 5, 4] and want[4] == 102 and want[6] == 0

@@ -48,12 +48,38 @@ def test_trait_error_mapping(cc, golden):
 
 
 def test_sign_and_pubkey_golden(golden):
+    """Golden keys are raw scalars: a context with OVH_FLAG_SK_RAW (blst SecretKey::from_bytes)."""
     import consensus_overlord_amd as coa
+    from consensus_overlord_amd.crypto import FLAG_SK_RAW, Context
+    ctx = Context(flags=FLAG_SK_RAW)
     for k, v in zip(golden["keys"][:4], golden["votes"][:4]):
-        c = coa.ConsensusCrypto(_b(k["sk"]))
+        c = coa.ConsensusCrypto(_b(k["sk"]), ctx=ctx)
         assert c.name.hex() == k["pk"]
         assert c.sign(_b(v["digest"])).hex() == v["sig"]
         assert c.hash(_b(v["rlp"])).hex() == v["digest"]
+
+
+def test_reference_example_private_key():
+    """ConsensusCrypto::new on the reference's own example/private_key (>= r): KeyGen parse,
+    name and signatures equal the oracle's fixture (tests/golden/example_key.json); the strict
+    scalar parse (OVH_FLAG_SK_RAW) rejects it with BLST_BAD_ENCODING."""
+    import json
+    import os
+    import consensus_overlord_amd as coa
+    from consensus_overlord_amd.crypto import FLAG_SK_RAW, Context, CryptoErr
+    with open(os.path.join(os.path.dirname(__file__), "golden", "example_key.json")) as fh:
+        ex = json.load(fh)
+    c = coa.ConsensusCrypto(ex["key_hex"] + "\n")      # the key file's text, as read from disk
+    assert c.scalar().hex() == ex["scalar"]
+    assert c.name.hex() == ex["name"]
+    for s in ex["signatures"]:
+        assert c.sign(_b(s["digest"])).hex() == s["sig"]
+        c.verify_signature(_b(s["sig"]), _b(s["digest"]), c.name)
+    try:
+        coa.ConsensusCrypto(ex["key_hex"], ctx=Context(flags=FLAG_SK_RAW))
+        raise AssertionError("strict parse accepted a key >= r")
+    except CryptoErr as e:
+        assert e.code == ex["raw_parse_code"]
 
 
 def test_aggregate_golden(cc, golden):
@@ -101,7 +127,7 @@ def test_batch_matches_per_vote_golden(cc, golden):
     cases = [c for c in golden["verify"] if len(_b(c["sig"])) == 96 and len(_b(c["hash"])) == 32
              and len(_b(c["pk"])) == 48]
     codes = cc.verify_batch([_b(c["sig"]) for c in cases], [_b(c["hash"]) for c in cases],
-                            [_b(c["pk"]) for c in cases], seed=7)
+                            [_b(c["pk"]) for c in cases])
     for c, got in zip(cases, codes):
         assert got == c["code"], c["name"]
 
@@ -109,7 +135,7 @@ def test_batch_matches_per_vote_golden(cc, golden):
 def test_batch_all_valid_uses_rlc(cc, golden):
     v = golden["votes"]
     k = golden["keys"]
-    codes = cc.verify_batch([_b(x["sig"]) for x in v], [_b(x["digest"]) for x in v], [_b(x["pk"]) for x in k], seed=1)
+    codes = cc.verify_batch([_b(x["sig"]) for x in v], [_b(x["digest"]) for x in v], [_b(x["pk"]) for x in k])
     assert list(codes) == [0] * len(v)
 
 
@@ -147,10 +173,10 @@ def test_device_batch_config5_invalid_positions(cc):
         s_host[i] = np.frombuffer(bls.g2_compress(bls.pt_add(bls.Fp2Ops, pt, bls.G2_GEN)), dtype=np.uint8)
     sigs2 = torch.from_numpy(s_host).cuda()
     torch.cuda.synchronize()
-    codes = dev.verify_batch(cc.ctx, sigs2, hs, pks, seed=99).cpu().numpy()
+    codes = dev.verify_batch(cc.ctx, sigs2, hs, pks).cpu().numpy()
     assert [i for i in range(n) if codes[i] != 0] == bad
     assert all(codes[i] == 5 for i in bad)
-    codes = dev.verify_batch(cc.ctx, sigs, hs, pks, seed=100).cpu().numpy()
+    codes = dev.verify_batch(cc.ctx, sigs, hs, pks).cpu().numpy()
     assert (codes == 0).all()
 
 
@@ -164,16 +190,20 @@ def test_partials_combine_two_shards(cc):
     parts = torch.empty((2, 864), dtype=torch.uint8, device="cuda")
     codes = torch.empty((n,), dtype=torch.int32, device="cuda")
     h = n // 2
-    dev.batch_partial(cc.ctx, sigs[:h], hs[:h], pks[:h], 11, codes[:h], parts[0])
-    dev.batch_partial(cc.ctx, sigs[h:], hs[h:], pks[h:], 12, codes[h:], parts[1])
+    dev.batch_partial(cc.ctx, sigs[:h], hs[:h], pks[:h], codes[:h], parts[0])
+    dev.batch_partial(cc.ctx, sigs[h:], hs[h:], pks[h:], codes[h:], parts[1])
     assert dev.combine_partials(cc.ctx, parts)
     # swap two hashes across shards: the combined check must fail
     hs2 = hs.clone()
     hs2[[0, h]] = hs[[h, 0]]
     torch.cuda.synchronize()
-    dev.batch_partial(cc.ctx, sigs[:h], hs2[:h], pks[:h], 11, codes[:h], parts[0])
-    dev.batch_partial(cc.ctx, sigs[h:], hs2[h:], pks[h:], 12, codes[h:], parts[1])
+    dev.batch_partial(cc.ctx, sigs[:h], hs2[:h], pks[:h], codes[:h], parts[0])
+    dev.batch_partial(cc.ctx, sigs[h:], hs2[h:], pks[h:], codes[h:], parts[1])
     assert not dev.combine_partials(cc.ctx, parts)
+    # the synchronous bisection of the last shard flags exactly its swapped vote
+    dev.batch_fallback(cc.ctx, n - h, codes[h:])
+    c = codes[h:].cpu().numpy()
+    assert [i for i in range(n - h) if c[i] != 0] == [0] and c[0] == 5
 
 
 def test_pipelined_batches_with_invalid(cc):
@@ -196,7 +226,7 @@ def test_pipelined_batches_with_invalid(cc):
     codes = torch.full((4, n), -1, dtype=torch.int32, device="cuda")
     torch.cuda.synchronize()
     for b, sg in enumerate((sigs, sigs_bad, sigs, sigs_bad)):
-        dev.verify_batch_async(cc.ctx, sg, hs, pks, 40 + b, codes[b])
+        dev.verify_batch_async(cc.ctx, sg, hs, pks, codes[b])
     dev.batch_wait(cc.ctx)
     c = codes.cpu().numpy()
     assert (c[0] == 0).all() and (c[2] == 0).all()
@@ -223,9 +253,9 @@ def test_pipelined_combine_async(cc):
         parts = torch.empty((2, 864), dtype=torch.uint8, device="cuda")
         c1 = torch.full((h,), -1, dtype=torch.int32, device="cuda")
         c0 = torch.full((h,), -1, dtype=torch.int32, device="cuda")
-        dev.batch_partial(cc.ctx, sigs[h:], hh[h:], pks[h:], 5, c1, parts[1])
-        dev.batch_partial(cc.ctx, sigs[:h], hh[:h], pks[:h], 6, c0, parts[0])
-        dev.combine_partials_async(cc.ctx, parts, h, c0)   # fallback for the last partial's shard
+        dev.batch_partial(cc.ctx, sigs[h:], hh[h:], pks[h:], c1, parts[1], stream=True)
+        dev.batch_partial(cc.ctx, sigs[:h], hh[:h], pks[:h], c0, parts[0], stream=True)
+        dev.combine_partials_async(cc.ctx, parts, h, c0, stream=True)   # bisection of the last shard
         dev.batch_wait(cc.ctx)
         out.append(c0.cpu().numpy())
     assert (out[0] == 0).all()
@@ -250,7 +280,7 @@ def test_partials_interoperate_with_oracle(cc):
         torch.cuda.synchronize()
         parts = torch.empty((2, 864), dtype=torch.uint8, device="cuda")
         codes = torch.empty((h,), dtype=torch.int32, device="cuda")
-        dev.batch_partial(cc.ctx, sigs[:h], hh[:h], pks[:h], 71, codes, parts[0])
+        dev.batch_partial(cc.ctx, sigs[:h], hh[:h], pks[:h], codes, parts[0])
         c1, p1 = orc.batch_partial(sigs[h:].cpu().numpy(), hh[h:].cpu().numpy(), pks[h:].cpu().numpy(), 72)
         assert (c1 == 0).all()
         parts[1] = torch.from_numpy(p1).cuda()
@@ -287,7 +317,7 @@ def test_shard_verifier_rccl_single_rank(cc):
         codes = torch.full((3, n), -1, dtype=torch.int32, device="cuda")
         torch.cuda.synchronize()
         for b, sg in enumerate((sigs, bad, sigs)):
-            sv.submit(b, sg, hs, pks, 1000 + b, codes[b])
+            sv.submit(b, sg, hs, pks, codes[b])
         sv.wait()
         c = codes.cpu().numpy()
         assert (c[0] == 0).all() and (c[2] == 0).all()

@@ -135,3 +135,47 @@ def test_golden_verify_codes(golden):
     for c in golden["verify"][:12]:
         code = ov.verify_signature(bytes.fromhex(c["sig"]), bytes.fromhex(c["hash"]), bytes.fromhex(c["pk"]))
         assert code == c["code"], c["name"]
+
+
+# ---- private-key parse: IETF KeyGen (ophelia-blst BlsPrivateKey::try_from [dep]) ----
+def test_hkdf_sha256_rfc5869_case1():
+    """RFC 5869 Appendix A.1 (the HKDF under KeyGen)."""
+    prk = bls.hkdf_extract(bytes(range(13)), b"\x0b" * 22)
+    assert prk.hex() == "077709362c2e32df0ddc3f0dc47bba6390b6c73bb50f9c3122ec844ad7c2b3e5"
+    okm = bls.hkdf_expand(prk, bytes(range(0xF0, 0xFA)), 42)
+    assert okm.hex() == ("3cb25f25faacd57a90434f64d0362f2a2d2d0a90cf1a5a4c5db02d56ecc4c5bf"
+                         "34007208d5b887185865")
+
+
+def test_keygen_eip2333_master_key():
+    """EIP-2333 test case 0: derive_master_SK(seed) = HKDF_mod_r(seed) = KeyGen(seed, "")."""
+    seed = bytes.fromhex("c55257c360c07c72029aebc1b53c05ed0362ada38ead3e3e9efa3708e53495531f09a6987599d182"
+                         "64c1e1c92f2cf141630c7a3c4ab7c81b2f001698e7463b04")
+    assert bls.sk_keygen(seed) == 6083874454709270928345386274498605044986640685124978867557563392430687146096
+    import orc
+    assert orc.sk_keygen(seed) == (0, bls.sk_keygen(seed).to_bytes(32, "big"))
+
+
+def test_example_private_key_fixture():
+    """The reference's example/private_key (>= r) parses by KeyGen; the fixture's name and
+    signatures follow from the oracle (tests/golden/make_example_key.py)."""
+    import json
+    import os
+    import orc
+    with open(os.path.join(os.path.dirname(__file__), "golden", "example_key.json")) as fh:
+        ex = json.load(fh)
+    key = bytes.fromhex(ex["key_hex"])
+    assert int.from_bytes(key, "big") >= bls.R
+    sk = bls.sk_keygen(key)
+    assert "%064x" % sk == ex["scalar"]
+    assert orc.sk_keygen(key) == (0, bytes.fromhex(ex["scalar"]))
+    assert bls.g1_compress(bls.sk_to_pk(sk)).hex() == ex["name"]
+    assert orc.sk_to_pk(sk.to_bytes(32, "big")) == (0, bytes.fromhex(ex["name"]))
+    for s in ex["signatures"]:
+        assert orc.sign(sk.to_bytes(32, "big"), bytes.fromhex(s["digest"])) == (0, bytes.fromhex(s["sig"]))
+    try:
+        bls.sk_from_bytes(key)
+        raise AssertionError("strict parse accepted a key >= r")
+    except bls.BlstError as e:
+        assert e.code == ex["raw_parse_code"]
+    assert orc.sk_keygen(key[:31])[0] == 1     # KeyGen needs >= 32 bytes of key material

@@ -2,7 +2,8 @@
 each rank verifying its shard of the golden votes with the C oracle as the compute backend
 (test infrastructure; the GPU backend is libovhip). Checks: per-rank codes equal the per-vote
 verdicts, the pipelined double-buffered partials, the combined verdict equals the single-process
-RLC batch, and a batch with one swapped signature falls back exactly on the owning shard."""
+RLC batch (one global vote index across the ranks), and a batch with one swapped signature falls
+back exactly on the owning shard."""
 import os
 import socket
 
@@ -17,15 +18,21 @@ from consensus_overlord_amd.shard import ShardVerifier, shard_bounds
 
 
 class OracleBackend:
+    """Test seeds (the device backend draws secret ones): batch s uses seed 0xC17A + s, vote i of
+    the whole batch SplitMix64(seed, i) -- the rank's shard offset is the index base."""
+
     def __init__(self):
         self.last = None
         self.verdicts = []
+        self.batch = 0
 
     def empty_partials(self, world):
         return torch.zeros((2, world, 864), dtype=torch.uint8)
 
-    def partial(self, sigs, hashes, pks, seed, codes, out_row):
-        c, part = orc.batch_partial(sigs.numpy(), hashes.numpy(), pks.numpy(), seed)
+    def partial(self, sigs, hashes, pks, codes, out_row, index_base):
+        seed = 0xC17A + self.batch
+        self.batch += 1
+        c, part = orc.batch_partial(sigs.numpy(), hashes.numpy(), pks.numpy(), seed, base=index_base)
         codes.copy_(torch.from_numpy(c))
         out_row.copy_(torch.from_numpy(part))
         self.last = (sigs.numpy(), hashes.numpy(), pks.numpy())
@@ -60,7 +67,7 @@ def _worker(rank, world, port, golden, q):
         lo, hi = shard_bounds(len(sg), world, rank)
         codes = torch.full((hi - lo,), -1, dtype=torch.int32)
         sv.submit(s, torch.from_numpy(sg[lo:hi].copy()), torch.from_numpy(hs[lo:hi].copy()),
-                  torch.from_numpy(pk[lo:hi].copy()), 0xC17A + s, codes)
+                  torch.from_numpy(pk[lo:hi].copy()), codes, index_base=lo)
         out.append(codes)
     sv.wait()
     got = [None] * world
@@ -96,3 +103,4 @@ def test_two_rank_gloo_shards(golden):
         ref_codes, ref_ok = orc.verify_batch_rlc(sg, hs, pk, seed=0xC17A + s)
         assert got[0][1][s] == got[1][1][s] == ref_ok == (s != 1)
         assert ref_codes.tolist() == want.tolist()
+

@@ -98,7 +98,28 @@ def test_vote_program_on_interpreter(hx, built, golden_votes, any_all):  # noqa:
 
 
 @pytest.mark.parametrize("any_all", [0, 1])
-def test_fold_final_pairchk_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
+def test_vote_t_program_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
+    """vote_t (key from the validator table, projective) on the golden votes: interpreter ==
+    simulator, and the same r sigma as the vote program."""
+    consts, progs_ = built
+    _, vsc, vwords, _, _ = progs_["vote"]
+    prog, sc, words, _, _ = progs_["vote_t"]
+    bls = gen._oracle()
+    with open(os.path.join(ROOT, "tests", "golden", "golden_v1.json")) as fh:
+        g = json.load(fh)
+    r = 0x0F1E2D3C4B5A6978
+    for k, inp in enumerate(golden_votes[:2]):
+        pk = bls.g1_from_bytes(bytes.fromhex(g["keys"][k]["pk"]))
+        tin = {n: inp[n] for n in ("sig_x0", "sig_x1", "sig_sort", "u00", "u01", "u10", "u11")}
+        tin.update(pk_X=pk[0] * 5 % P, pk_Y=pk[1] * 5 % P, pk_Z=5)
+        sim = sched.simulate(sc, words, tin, r)
+        assert_same(run_vm(hx, consts, sc, words, tin, r, any_all), sim, "vote_t %d" % k)
+        vsim = sched.simulate(vsc, vwords, inp, r)
+        assert [sim["st:s%d" % j] for j in range(6)] == [vsim["st:s%d" % j] for j in range(6)]
+
+
+@pytest.mark.parametrize("any_all", [0, 1])
+def test_fold_final_bisect_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
     consts, progs_ = built
     prog, sc, words, _, _ = progs_["vote"]
     r = 0x1234567890ABCDEF
@@ -107,20 +128,26 @@ def test_fold_final_pairchk_on_interpreter(hx, built, golden_votes, any_all):  #
         o = sched.simulate(sc, words, inp, r)
         o = {(n[3:] if n.startswith("st:") else n): v for n, v in o.items()}
         parts.append(o)
-    inp = {}
-    for k in range(progs.FOLD_K):
-        for j in range(12):
-            inp["F%d_%d" % (k, j)] = parts[k]["f%d" % j] if k < 2 else (1 if j == 0 else 0)
-        for j in range(6):
-            inp["S%d_%d" % (k, j)] = parts[k]["s%d" % j] if k < 2 else (1 if j == 2 else 0)
+
+    def final_in(items):
+        inp = {}
+        for k in range(progs.FOLD_K):
+            for j in range(12):
+                inp["F%d_%d" % (k, j)] = items[k][0]["f%d" % j] if k < len(items) else (1 if j == 0 else 0)
+            for j in range(6):
+                inp["S%d_%d" % (k, j)] = items[k][1]["s%d" % j] if k < len(items) else (1 if j == 2 else 0)
+        return inp
+    inp = final_in([(parts[0], parts[0]), (parts[1], parts[1])])
     for name in ("fold", "final"):
         _, psc, pwords, _, _ = progs_[name]
         sim = sched.simulate(psc, pwords, inp)
         assert_same(run_vm(hx, consts, psc, pwords, inp, 0, any_all), sim, name)
         if name == "final":
             assert sim == {"ok": 1}
-    _, psc, pwords, _, _ = progs_["pairchk"]
-    pin = {n: parts[0][n] for n in progs.PAIRCHK_IN}
-    sim = sched.simulate(psc, pwords, pin)
-    assert sim == {"ok": 1}
-    assert_same(run_vm(hx, consts, psc, pwords, pin, 0, any_all), sim, "pairchk")
+    # the bisection's per-vote check: one vote's own (f, r sigma) passes, a mismatched pair fails
+    _, psc, pwords, _, _ = progs_["final"]
+    for items, want in (([(parts[0], parts[0])], 1), ([(parts[0], parts[1])], 0)):
+        pin = final_in(items)
+        sim = sched.simulate(psc, pwords, pin)
+        assert sim == {"ok": want}
+        assert_same(run_vm(hx, consts, psc, pwords, pin, 0, any_all), sim, "final/bisect")

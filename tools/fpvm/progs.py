@@ -3,10 +3,13 @@ layouts. Input and output names are listed in the order the HIP side addresses t
 
   vote     one vote of ovh_verify_batch: pk decompress + G1 subgroup
            check, sig decompress + G2 subgroup check, hash_to_G2 from (u0, u1), the RLC
-           scalar products r pk (affine) and r sigma (projective), f = Miller(r pk, H).
+           scalar products r pk and r sigma (projective), f = Miller(r pk, H).
+  vote_t   the same for a public key taken from the device validator table (ovh_set_validators:
+           already decompressed and group-checked, projective) or a QC's aggregated key.
   fold     4 partials (F_i in Fp12, S_i projective G2) -> (prod F_i, sum S_i)
-  final    up to 4 partials -> prod F * Miller(-G1, sum S) -> final exponentiation == 1
-  pairchk  per-vote fallback: e(pk, H) == e(G1, sigma)
+  final    up to 4 partials -> prod F * Miller(-G1, sum S) -> final exponentiation == 1; also
+           the bisection checks of the fallback (one group's partial, or one vote's (f, r sigma):
+           e(r pk, H) e(-G1, r sigma) = (e(pk, H) / e(G1, sigma))^r == 1 iff the vote verifies).
 """
 from __future__ import annotations
 
@@ -44,14 +47,13 @@ def unflat_g2p(v):
 
 
 # HBM state planes of a vote (ovhip.hip reads them through VM_S_* in vm_progs.inc)
-S_U, S_FB, S_RS, S_F, S_TOTAL = 0, 4, 16, 22, 34
+S_U, S_RS, S_F, S_TOTAL = 0, 4, 10, 22
 
 VOTE_IN = ["pk_x", "pk_sort", "sig_x0", "sig_x1", "sig_sort", "u00", "u01", "u10", "u11"]
 VOTE_OUT = ["pk_ok", "pk_grp", "sig_ok", "sig_grp", "h_inf"]
 # stored straight to HBM planes by `st` ops as soon as they are final
 VOTE_ST = [(n, S_F + k) for k, n in enumerate(f12_names("f"))] + \
-    [(n, S_RS + k) for k, n in enumerate(g2p_names("s"))] + \
-    [(n, S_FB + k) for k, n in enumerate(["pkx", "pky", "sx0", "sx1", "sy0", "sy1"] + g2p_names("h"))]
+    [(n, S_RS + k) for k, n in enumerate(g2p_names("s"))]
 
 
 def build_vote():
@@ -75,8 +77,34 @@ def build_vote():
     f = a.miller_loop(rP, H)
     for name, v in zip(VOTE_OUT, [pk_ok, pk_grp, sig_ok, sig_grp, h_inf]):
         p.output(name, v)
-    stv = flat12(f) + flat_g2p(rS) + [px, py, qx[0], qx[1], qy[0], qy[1]] + flat_g2p(H)
-    for (name, plane), v in zip(VOTE_ST, stv):
+    for (name, plane), v in zip(VOTE_ST, flat12(f) + flat_g2p(rS)):
+        p.store(name, v, plane)
+    return p
+
+
+VOTE_T_IN = ["pk_X", "pk_Y", "pk_Z", "sig_x0", "sig_x1", "sig_sort", "u00", "u01", "u10", "u11"]
+VOTE_T_OUT = ["sig_ok", "sig_grp", "h_inf"]
+
+
+def build_vote_t():
+    p = Prog("vote_t")
+    a = Alg(p, use_sop=USE_SOP)
+    R = p.const(R_MONT)
+    Pp = (p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z"))
+    sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
+    u0 = (p.input("u00"), p.input("u01"))
+    u1 = (p.input("u10"), p.input("u11"))
+    sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
+    Qs = (qx, qy, (p.one, p.zero))
+    sig_grp = a.g2_in_group(Qs)
+    H = a.hash_to_g2(u0, u1)
+    h_inf = a.f2_is_zero(H[2])
+    rP = a.pt_mul_glv("fp", Pp, a.g1_phi(Pp))
+    rS = a.pt_mul_glv("f2", Qs, a.g2_neg_psi2(Qs))
+    f = a.miller_loop(rP, H)
+    for name, v in zip(VOTE_T_OUT, [sig_ok, sig_grp, h_inf]):
+        p.output(name, v)
+    for (name, plane), v in zip(VOTE_ST, flat12(f) + flat_g2p(rS)):
         p.store(name, v, plane)
     return p
 
@@ -127,26 +155,9 @@ def build_final():
     return p
 
 
-PAIRCHK_IN = ["pkx", "pky", "sx0", "sx1", "sy0", "sy1"] + g2p_names("h")
-PAIRCHK_OUT = ["ok"]
-
-
-def build_pairchk():
-    p = Prog("pairchk")
-    a = Alg(p, use_sop=USE_SOP)
-    pk = (p.input("pkx"), p.input("pky"))
-    sig = ((p.input("sx0"), p.input("sx1")), (p.input("sy0"), p.input("sy1")), (p.one, p.zero))
-    H = unflat_g2p([p.input(n) for n in g2p_names("h")])
-    f1 = a.miller_loop(pk, H)
-    ng1 = (p.const(G1X), p.const(-G1Y))
-    f2 = a.miller_loop(ng1, sig)
-    p.output("ok", a.f12_eq_one(a.final_exp(a.f12_mul(f1, f2))))
-    return p
-
-
 PROGRAMS = {
     "vote": (build_vote, VOTE_IN, VOTE_OUT),
+    "vote_t": (build_vote_t, VOTE_T_IN, VOTE_T_OUT),
     "fold": (build_fold, FOLD_IN, FOLD_OUT),
     "final": (build_final, FINAL_IN, FINAL_OUT),
-    "pairchk": (build_pairchk, PAIRCHK_IN, PAIRCHK_OUT),
 }
