@@ -90,8 +90,11 @@ def test_prefetch_then_serial_verify_hits_cache(golden):
     h1, m1, _ = c.cache_stats()
     assert h1 - h0 == len(cases) and m1 == m0
     # a triple not prefetched is a miss and still exact
-    c.verify_signature(sigs[0], hs[0], pks[0])
-    assert c.lib.ovh_verify(c.ctx.ptr, sigs[1], 96, hs[0], 32, pks[0], 48) == 5
+    import orc
+    v = [x for x in cases if x["name"].startswith("valid_")]
+    s2, h3, p4 = _b(v[2]["sig"]), _b(v[3]["hash"]), _b(v[4]["pk"])
+    assert (s2, h3, p4) not in set(zip(sigs, hs, pks))
+    assert c.lib.ovh_verify(c.ctx.ptr, s2, 96, h3, 32, p4, 48) == orc.verify(s2, h3, p4) == 5
     assert c.cache_stats()[1] == m1 + 1
 
 
