@@ -4,8 +4,16 @@
 //
 // LDS holds each slice's register file: `nslots` Fp slots of 12 x u32 (48 B, read and written
 // as three ds_*_b128), plus the shared constant table. In every phase each lane runs at most
-// one op (the generator's schedule) and the workgroup barrier makes its result visible to the
-// next phase. Opcodes and operand encoding: tools/fpvm/sched.py.
+// one op (the generator's schedule); a slot written in phase t is read from phase t + 1 on.
+// Opcodes and operand encoding: tools/fpvm/sched.py.
+//
+// Lazy reduction. A slot holds a Montgomery representative in [0, 2p) (p < 2^381, so 2^384 >
+// 9.8 p leaves room): products take operands in [0, 4p) -- a + b or a + (2p - b) of two slots,
+// with no reduction -- and return [0, 1.625 p) after one conditional subtraction
+// ((4p)^2 / 2^384 + p < 2.63 p); linear combinations sum their terms unreduced (< 8p, times
+// k <= 15 < 120p) and reduce once by a float estimate of the quotient to [0, 2p). Only the ops
+// whose result depends on the canonical value (sgn0, lex, the equality test, `st` outputs,
+// inversion) canonicalise: a product by the plain 1 of a value below 4p is at most p.
 #pragma once
 #include "bls/fp.hpp"
 
@@ -29,6 +37,9 @@ enum : uint32_t {
   OP_AND = 8, OP_OR = 9, OP_XOR = 10, OP_ST = 11, OP_SELB = 12,
 };
 
+// phases of instruction prefetch (the uploaded code carries this many trailing NOP phases)
+constexpr uint32_t PREFETCH = 4;
+
 // Where `st` ops write: plane `imm` of unit `unit` in a structure-of-arrays slab (limb k of
 // plane j at base[(j * 12 + k) * cap + unit]).
 struct Out {
@@ -39,7 +50,7 @@ struct Out {
 constexpr uint32_t CONST_BASE = 0x800;
 
 VM_FN void ld_slot(Fp& r, const uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
-                                        uint32_t ref) {
+                   uint32_t ref) {
   const uint32_t* src = ref >= CONST_BASE ? cst + (ref - CONST_BASE) * 12 : slots + ref * 12;
   const uint4* s4 = reinterpret_cast<const uint4*>(src);
   const uint4 a = s4[0], b = s4[1], c = s4[2];
@@ -60,6 +71,41 @@ VM_FN void set_flag(Fp& z, uint32_t f) {
   z.v[0] = f;
 }
 
+// 2p as 12 limbs (2p < 2^382)
+constexpr uint32_t P2_LIMBS[12] = {
+    P_LIMBS[0] << 1, (P_LIMBS[1] << 1) | (P_LIMBS[0] >> 31), (P_LIMBS[2] << 1) | (P_LIMBS[1] >> 31),
+    (P_LIMBS[3] << 1) | (P_LIMBS[2] >> 31), (P_LIMBS[4] << 1) | (P_LIMBS[3] >> 31),
+    (P_LIMBS[5] << 1) | (P_LIMBS[4] >> 31), (P_LIMBS[6] << 1) | (P_LIMBS[5] >> 31),
+    (P_LIMBS[7] << 1) | (P_LIMBS[6] >> 31), (P_LIMBS[8] << 1) | (P_LIMBS[7] >> 31),
+    (P_LIMBS[9] << 1) | (P_LIMBS[8] >> 31), (P_LIMBS[10] << 1) | (P_LIMBS[9] >> 31),
+    (P_LIMBS[11] << 1) | (P_LIMBS[10] >> 31)};
+
+// [0, 2p) -> [0, p): one conditional subtraction
+VM_FN void canon(Fp& r, const Fp& a) {
+  uint32_t d[12], br = 0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) d[j] = subc32(a.v[j], P_LIMBS[j], br, &br);
+#pragma unroll
+  for (int j = 0; j < 12; ++j) r.v[j] = br ? a.v[j] : d[j];
+}
+
+// s (13 limbs, s < 2^389) -> r in [0, 2p), r == s mod p. With T = s >> 359 (< 2^30) and
+// Pt = p >> 359, T / (Pt + 1) <= s / p < (T + 1) / Pt, and s / p - T / (Pt + 1) < 3e-4 for
+// s < 248 p; the f32 quotient is shrunk by 2^-20 (three f32 roundings stay below it), so
+// q = floor(f) is floor(s / p) or one less: s - q p lies in [0, 2p).
+VM_FN void reduce2p(Fp& r, const uint32_t* s) {
+  const uint32_t t = (uint32_t)((((uint64_t)s[12] << 32) | s[11]) >> 7);
+  constexpr float QS = (float)((1.0 - 0x1p-20) / (double)((P_LIMBS[11] >> 7) + 1));
+  const uint32_t q = (uint32_t)((float)t * QS);
+  uint64_t pr = 0;
+  uint32_t br = 0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    pr = (uint64_t)P_LIMBS[j] * q + (pr >> 32);
+    r.v[j] = subc32(s[j], (uint32_t)pr, br, &br);
+  }
+}
+
 // acc (13 limbs) += c * X for |c| <= 15, branch-free on the coefficient's value and sign.
 VM_FN void acc_term(uint32_t* acc, const Fp& X, int c) {
   const uint32_t k = c < 0 ? (uint32_t)(-c) : (uint32_t)c;
@@ -74,63 +120,78 @@ VM_FN void acc_term(uint32_t* acc, const Fp& X, int c) {
   acc[12] = acc[12] + ((uint32_t)(pr >> 32) ^ mask) + cy;
 }
 
-// acc = 2^k p (k = 5: 32 p, k = 6: 64 p), 13 limbs: the bias that keeps a signed sum >= 0
-VM_FN void acc_bias(uint32_t* acc, int k) {
+// acc = 128 p (13 limbs): the bias that keeps a signed sum of four |c| <= 15 terms >= 0
+VM_FN void acc_bias128(uint32_t* acc) {
   uint32_t prev = 0;
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    acc[j] = (P_LIMBS[j] << k) | (prev >> (32 - k));
+    acc[j] = (P_LIMBS[j] << 7) | (prev >> 25);
     prev = P_LIMBS[j];
   }
-  acc[12] = prev >> (32 - k);
+  acc[12] = prev >> 25;
 }
 
-// acc in [0, 128 p) -> acc mod p. With top = acc >> 352 and p_top = p >> 352, the ratio
-// r = top / (p_top + 1) has floor(r) = floor(acc / p) or one less. The f32 quotient f below
-// carries a relative error < 3 * 2^-24 and is shrunk by 2^-20, so f <= r and
-// floor(f) >= floor(r) - 1: q = floor(f) is at most floor(acc / p) and at most 2 short of it.
-// Subtract q p, then two conditional subtractions.
-// 2p as 12 limbs + a top limb
-constexpr uint32_t P2_LIMBS[12] = {
-    P_LIMBS[0] << 1, (P_LIMBS[1] << 1) | (P_LIMBS[0] >> 31), (P_LIMBS[2] << 1) | (P_LIMBS[1] >> 31),
-    (P_LIMBS[3] << 1) | (P_LIMBS[2] >> 31), (P_LIMBS[4] << 1) | (P_LIMBS[3] >> 31),
-    (P_LIMBS[5] << 1) | (P_LIMBS[4] >> 31), (P_LIMBS[6] << 1) | (P_LIMBS[5] >> 31),
-    (P_LIMBS[7] << 1) | (P_LIMBS[6] >> 31), (P_LIMBS[8] << 1) | (P_LIMBS[7] >> 31),
-    (P_LIMBS[9] << 1) | (P_LIMBS[8] >> 31), (P_LIMBS[10] << 1) | (P_LIMBS[9] >> 31),
-    (P_LIMBS[11] << 1) | (P_LIMBS[10] >> 31)};
-constexpr uint32_t P2_TOP = P_LIMBS[11] >> 31;
+// d = a + (neg ? 2p - b : b) for two independent (a, b) pairs, carry chains interleaved limb by
+// limb (gfx950 charges wait states for a VALU carry read right after its write).
+VM_FN void add_negsel2(Fp& x, const Fp& A, const Fp& B, bool nx, Fp& y, const Fp& C, const Fp& D, bool ny) {
+  uint32_t nb[12], nd[12], b1 = 0, b2 = 0, c1 = 0, c2 = 0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    nb[j] = subc32(P2_LIMBS[j], B.v[j], b1, &b1);
+    nd[j] = subc32(P2_LIMBS[j], D.v[j], b2, &b2);
+  }
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    x.v[j] = addc32(A.v[j], nx ? nb[j] : B.v[j], c1, &c1);
+    y.v[j] = addc32(C.v[j], ny ? nd[j] : D.v[j], c2, &c2);
+  }
+}
 
-VM_FN void acc_reduce(Fp& r, uint32_t* acc) {
-  const uint64_t top = ((uint64_t)acc[12] << 32) | acc[11];  // acc >> 352
-  constexpr float QS = (float)((1.0 - 0x1p-20) / ((double)P_LIMBS[11] + 1.0));
-  const uint32_t q = (uint32_t)((float)top * QS);
-  uint64_t pr = 0;
-  uint32_t br = 0;
+VM_FN void add2(Fp& x, const Fp& A, const Fp& B, Fp& y, const Fp& C, const Fp& D) {
+  uint32_t c1 = 0, c2 = 0;
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    pr = (uint64_t)P_LIMBS[j] * q + (pr >> 32);
-    acc[j] = subc32(acc[j], (uint32_t)pr, br, &br);
+    x.v[j] = addc32(A.v[j], B.v[j], c1, &c1);
+    y.v[j] = addc32(C.v[j], D.v[j], c2, &c2);
   }
-  acc[12] = acc[12] - (uint32_t)(pr >> 32) - br;
-  // acc is now below 3p: acc - p and acc - 2p as two interleaved borrow chains, keep the
-  // smallest non-negative of acc, acc - p, acc - 2p
-  uint32_t d1[13], d2[13], b1 = 0, b2 = 0;
+}
+
+// Product operands x = A + (nx ? 2p - B : B), y = C + (ny ? 2p - D : D) in [0, 4p), no
+// reduction. The negations' borrow chains run only when some lane of the wave has one
+// (`any_neg`); both paths write x, y in full (no register copies at the join).
+VM_FN void pre_add2(Fp& x, const Fp& A, const Fp& B, bool nx, Fp& y, const Fp& C, const Fp& D, bool ny,
+                    bool any_neg) {
+  if (any_neg) add_negsel2(x, A, B, nx, y, C, D, ny);
+  else add2(x, A, B, y, C, D);
+}
+
+// s = A + sb B + sc C + sd D with unit signs (a zero coefficient points its operand at the zero
+// constant): every negated term enters as 2p - X, so s < 8p fits 12 limbs. `any_neg`: some
+// lane of the wave negates a term.
+VM_FN void lin_sum(uint32_t* s, const Fp& A, const Fp& B, const Fp& C, const Fp& D, int sb, int sc, int sd,
+                   bool any_neg) {
+  Fp u, v;
+  if (any_neg) {
+    // (A + B') and (C' + D') as two chains: C' = 2p - C needs its own borrow chain first
+    uint32_t nc[12], b3 = 0;
 #pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    d1[j] = subc32(acc[j], P_LIMBS[j], b1, &b1);
-    d2[j] = subc32(acc[j], P2_LIMBS[j], b2, &b2);
+    for (int j = 0; j < 12; ++j) nc[j] = subc32(P2_LIMBS[j], C.v[j], b3, &b3);
+    Fp c;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) c.v[j] = sc < 0 ? nc[j] : C.v[j];
+    add_negsel2(u, A, B, sb < 0, v, c, D, sd < 0);
+  } else {
+    add2(u, A, B, v, C, D);
   }
-  d1[12] = subc32(acc[12], 0u, b1, &b1);
-  d2[12] = subc32(acc[12], P2_TOP, b2, &b2);
+  uint32_t c3 = 0;
 #pragma unroll
-  for (int j = 0; j < 13; ++j) acc[j] = !b2 ? d2[j] : (!b1 ? d1[j] : acc[j]);
-#pragma unroll
-  for (int j = 0; j < 12; ++j) r.v[j] = acc[j];
+  for (int j = 0; j < 12; ++j) s[j] = addc32(u.v[j], v.v[j], c3, &c3);
+  s[12] = 0;
 }
 
 // Modular inverse of a Montgomery value by the binary extended Euclidean algorithm on the
 // raw representation (the inputs are public batch data: variable time is fine), then back to
-// Montgomery form with one product by raw R^3 (r3). 0 -> 0.
+// Montgomery form with one product by raw R^3 (r3). 0 -> 0. `a` must be canonical.
 VM_FN bool limbs_is_one(const Fp& w) {
   uint32_t acc = w.v[0] ^ 1u;
 #pragma unroll
@@ -185,53 +246,6 @@ VM_FN void fp_inv_binary(Fp& r, const Fp& a, const Fp& r3) {
   fp_mul(r, limbs_is_one(u) ? x1 : x2, r3);
 }
 
-// r = A + s B mod p for s in {-1, 0, +1} (A, B < p; the encoder points B at the zero
-// constant when s = 0), branch-free: d = A + (s < 0 ? p - B : B) < 2p, then one conditional
-// subtraction of p.
-VM_FN void addsub(Fp& r, const Fp& A, const Fp& B, int s) {
-  // the three carry chains (p - B, A + B', d - p) run skewed by one limb each and interleave, so
-  // no chain's carry read directly follows its own carry write (gfx950 wait states)
-  uint32_t nb[12], d[12], t[12], b0 = 0, c1 = 0, b2 = 0;
-  const bool ng = s < 0;
-#pragma unroll
-  for (int j = 0; j < 14; ++j) {
-    if (j < 12) nb[j] = subc32(P_LIMBS[j], B.v[j], b0, &b0);
-    if (j >= 1 && j <= 12) d[j - 1] = addc32(A.v[j - 1], ng ? nb[j - 1] : B.v[j - 1], c1, &c1);
-    if (j >= 2) t[j - 2] = subc32(d[j - 2], P_LIMBS[j - 2], b2, &b2);
-  }
-#pragma unroll
-  for (int j = 0; j < 12; ++j) r.v[j] = b2 ? d[j] : t[j];
-}
-
-// Two independent addsubs with their carry chains interleaved limb by limb: on gfx950 a VALU
-// carry read right after the VALU carry write costs wait states (s_nop), which the other
-// chain's instruction fills.
-VM_FN void addsub2(Fp& r1, const Fp& A1, const Fp& B1, int s1, Fp& r2, const Fp& A2, const Fp& B2, int s2) {
-  uint32_t n1[12], n2[12], d1[12], d2[12], t1[12], t2[12], b1 = 0, b2 = 0, c1 = 0, c2 = 0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    n1[j] = subc32(P_LIMBS[j], B1.v[j], b1, &b1);
-    n2[j] = subc32(P_LIMBS[j], B2.v[j], b2, &b2);
-  }
-  const bool g1 = s1 < 0, g2 = s2 < 0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    d1[j] = addc32(A1.v[j], g1 ? n1[j] : B1.v[j], c1, &c1);
-    d2[j] = addc32(A2.v[j], g2 ? n2[j] : B2.v[j], c2, &c2);
-  }
-  b1 = b2 = 0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    t1[j] = subc32(d1[j], P_LIMBS[j], b1, &b1);
-    t2[j] = subc32(d2[j], P_LIMBS[j], b2, &b2);
-  }
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    r1.v[j] = b1 ? d1[j] : t1[j];
-    r2.v[j] = b2 ? d2[j] : t2[j];
-  }
-}
-
 #if defined(__HIPCC__)
 VM_FN bool wave_any(bool p) { return __ballot(p) != 0; }
 #else
@@ -241,14 +255,15 @@ extern bool g_host_any;
 inline bool wave_any(bool p) { return p || g_host_any; }
 #endif
 
-// One phase of one lane. `in` = (w0, A|B<<16, C|D<<16, coefficients). The common ops share one
-// straight-line body: x = A + cb B, y = C + cc cd D (unit coefficients, tools/fpvm/ir.lin_form),
-// then fp_mul(x, y) (muls / sgn0 / lex), x == y (eq) or k (x + cc y) (lin). Each block runs
-// when any lane of the wave needs it (a wave-uniform branch) and every lane keeps the result
-// of its own op. Rare ops (sel, selb, logic, st, inv, lin with general coefficients) take
-// per-lane branches after that.
-VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots,
-                                     const uint32_t* __restrict__ cst, uint64_t scalar, const Out& out) {
+// One phase of one lane. `in` = (w0, A|B<<16, C|D<<16, coefficients). The common ops run behind
+// wave-uniform branches (a block runs when any lane of the wave needs it) and each lane stores
+// the result of its own op:
+//   products  x = A + cb B, y = C + cd D (unit signs), m = x y: muls; sgn0 / lex / eq take the
+//             from-Montgomery product (y = plain 1; eq: x = A - B) and flag its canonical value;
+//   lin       k (A + cb B + cc C + cd D), unit signs, 1 <= k <= 15;
+//   rare      sel, selb, logic, st, inv, lin with general coefficients (per-lane branches).
+VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
+                uint64_t scalar, const Out& out) {
   const uint32_t op = active ? (in.x & 31) : (uint32_t)OP_NOP;
   if (!wave_any(op != OP_NOP)) return;
   const uint32_t dst = (in.x >> 5) & 0x7FF;
@@ -264,49 +279,47 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots,
   const bool is_mul = op == OP_MULS || op == OP_SGN0 || op == OP_LEX || op == OP_EQ;
   const bool lin_unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1;
   const bool is_lin = op == OP_LIN && lin_unit;
-  Fp z = A;
-  if (wave_any(is_mul || is_lin)) {
-    Fp x, y;
-    addsub2(x, A, B, cb, y, C, D, cc * cd);
-    if (wave_any(is_mul)) {
-      Fp m;
-      fp_mul(m, x, y);
-      const bool flag = is_mul && op != OP_MULS;
-      if (wave_any(flag)) {
-        uint32_t f = 0;
-        if (op == OP_SGN0) f = m.v[0] & 1u;
-        if (op == OP_LEX) f = limbs_gt(m.v, HALF_P) ? 1u : 0u;
-        if (op == OP_EQ) f = fp_eq(x, y) ? 1u : 0u;
+  if (wave_any(is_mul)) {
+    Fp x, y, m;
+    pre_add2(x, A, B, cb < 0, y, C, D, cd < 0, wave_any(is_mul && (cb < 0 || cd < 0)));
+    fp_mul(m, x, y);
+    const bool flag = is_mul && op != OP_MULS;
+    if (wave_any(flag)) {  // m is canonical here: y = 1, x < 4p -> x / 2^384 + p rounds to <= p
+      uint32_t f = 0;
+      if (op == OP_SGN0) f = m.v[0] & 1u;
+      if (op == OP_LEX) f = limbs_gt(m.v, HALF_P) ? 1u : 0u;
+      if (op == OP_EQ) f = fp_is_zero(m) ? 1u : 0u;
 #pragma unroll
-        for (int j = 0; j < 12; ++j) m.v[j] = flag ? (j == 0 ? f : 0u) : m.v[j];
-      }
-      if (is_mul) z = m;
+      for (int j = 0; j < 12; ++j) m.v[j] = flag ? (j == 0 ? f : 0u) : m.v[j];
     }
-    if (wave_any(is_lin)) {
-      Fp l;
-      addsub(l, x, y, cc);
-      const uint32_t k = (in.w >> 20) & 15;
-      if (wave_any(is_lin && k > 1)) {  // "scaled" form: k * (unit sum), k < 16 (k <= 1: unchanged)
-        uint32_t acc[13];
-        uint64_t pr = 0;
-        const uint32_t kk = k > 1 ? k : 1u;
+    if (is_mul) st_slot(slots, dst, m);
+  }
+  if (wave_any(is_lin)) {
+    uint32_t s[13];
+    lin_sum(s, A, B, C, D, cb, cc, cd, wave_any(is_lin && (cb < 0 || cc < 0 || cd < 0)));
+    const uint32_t k = (in.w >> 20) & 15;
+    if (wave_any(is_lin && k > 1)) {  // "scaled" form: k * (unit sum), k < 16 (k <= 1: unchanged)
+      const uint32_t kk = k > 1 ? k : 1u;
+      uint64_t pr = 0;
 #pragma unroll
-        for (int j = 0; j < 12; ++j) {
-          pr = (uint64_t)l.v[j] * kk + (pr >> 32);
-          acc[j] = (uint32_t)pr;
-        }
-        acc[12] = (uint32_t)(pr >> 32);
-        acc_reduce(l, acc);
+      for (int j = 0; j < 12; ++j) {
+        pr = (uint64_t)s[j] * kk + (pr >> 32);
+        s[j] = (uint32_t)pr;
       }
-      if (is_lin) z = l;
+      s[12] = (uint32_t)(pr >> 32);
     }
+    Fp l;
+    reduce2p(l, s);
+    if (is_lin) st_slot(slots, dst, l);
   }
   const bool rare = op != OP_NOP && !is_mul && !is_lin;
   if (wave_any(rare)) {
+    Fp z = A;
     if (op == OP_ST) {
+      canon(z, A);
       uint32_t* b = out.base + (size_t)imm * 12 * out.cap + out.unit;
 #pragma unroll
-      for (int k = 0; k < 12; ++k) b[(size_t)k * out.cap] = A.v[k];
+      for (int k = 0; k < 12; ++k) b[(size_t)k * out.cap] = z.v[k];
     } else if (op == OP_SELB) {
       z = ((scalar >> imm) & 1) ? C : B;
     } else if (op == OP_SEL) {
@@ -315,43 +328,54 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots,
       set_flag(z, op == OP_AND ? (A.v[0] & C.v[0]) : op == OP_OR ? (A.v[0] | C.v[0]) : (A.v[0] ^ C.v[0]));
     } else if (op == OP_INV) {
 #ifndef OVH_VM_NO_INV
-      fp_inv_binary(z, A, C);
+      Fp a;
+      canon(a, A);
+      fp_inv_binary(z, a, C);
 #endif
-    } else if (op == OP_LIN && !lin_unit) {  // general coefficients
+    } else if (op == OP_LIN) {  // general coefficients
       uint32_t acc[13];
-      acc_bias(acc, 6);
+      acc_bias128(acc);
       acc_term(acc, A, ca);
       acc_term(acc, B, cb);
       acc_term(acc, C, cc);
       acc_term(acc, D, cd);
-      acc_reduce(z, acc);
+      reduce2p(z, acc);
     }
+    if (rare && op != OP_ST) st_slot(slots, dst, z);
   }
-  if (op != OP_NOP && op != OP_ST) st_slot(slots, dst, z);
 }
 
-// Run `nphases` phases of a W-lane program. Every lane of the workgroup must call this (the
-// phase barrier is a workgroup barrier); lanes of inactive slices pass active = false.
+// Run `nphases` phases of a W-lane program. Every lane of the workgroup must call this; lanes
+// of inactive slices pass active = false. The VM kernels are single-wave workgroups, so no
+// phase barrier is needed: a wave's LDS operations are performed in issue order, and a slot a
+// phase writes is read from the next phase on (tools/fpvm/sched.py), so the next phase's loads
+// may issue while this phase's stores are still in flight.
 #if defined(__HIPCC__)
 __device__ __forceinline__ void run(const uint4* __restrict__ code, uint32_t nphases, uint32_t W, uint32_t lane,
                                     bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
                                     uint64_t scalar, const Out& out, uint64_t* __restrict__ trace = nullptr) {
-  // trace (diagnostics, OVH_FLAG_VM_TRACE): wall clock after every phase barrier
+  static_assert(PREFETCH == 4, "prefetch ring below is 4 deep");
+  // trace (diagnostics, OVH_FLAG_VM_TRACE): wall clock after every phase
   if (trace && threadIdx.x == 0) trace[0] = wall_clock64();
-  // instructions are prefetched two phases ahead (an HBM/L2 round trip outlasts a light phase)
-  uint4 nxt = code[lane], nxt2 = code[(size_t)W + lane];
+  // instructions are prefetched PREFETCH phases ahead (an HBM / L2 round trip outlasts a light
+  // phase); the code carries PREFETCH trailing NOP phases
+  uint4 q0 = code[lane], q1 = code[(size_t)W + lane], q2 = code[(size_t)2 * W + lane],
+        q3 = code[(size_t)3 * W + lane];
 #pragma unroll 1
   for (uint32_t ph = 0; ph < nphases; ++ph) {
-    const uint4 cur = nxt;
-    nxt = nxt2;
-    nxt2 = code[(size_t)(ph + 2) * W + lane];  // code carries two trailing NOP phases
+    const uint4 cur = q0;
+    q0 = q1;
+    q1 = q2;
+    q2 = q3;
+    q3 = code[(size_t)(ph + PREFETCH) * W + lane];
     exec(cur, active, slots, cst, scalar, out);
-    // The VM kernels are single-wave workgroups: the phase's slot writes are visible to the
-    // next phase's reads once this wave's LDS operations completed (lgkmcnt(0)); the barrier
-    // is kept for ordering but no longer waits for the instruction prefetch / HBM stores.
-    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (trace && threadIdx.x == 0) trace[ph + 1] = wall_clock64();
+    if (trace) {
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (threadIdx.x == 0) trace[ph + 1] = wall_clock64();
+    }
   }
+  // the caller reads results through LDS (other lanes' slots) and may reuse it
+  __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 #endif  // __HIPCC__

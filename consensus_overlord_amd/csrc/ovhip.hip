@@ -226,6 +226,7 @@ __device__ __forceinline__ void fold_unit(uint32_t t, uint32_t m, const VmDev& p
       Fp v;
       const uint32_t src = VM_FOLD_OUT[k];
       for (int q = 0; q < 12; ++q) v.v[q] = slots[src * 12 + q];
+      vm::canon(v, v);  // slots hold [0, 2p) representatives (fpvm.hpp); planes are canonical
       out.st(v, k, t);
     }
   }
@@ -820,7 +821,7 @@ static_assert(VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_NSLOTS * 12 + 4) &&
 
 static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphases, uint32_t W, const uint16_t* in,
                      uint32_t nin, const uint16_t* out, uint32_t nout) {
-  const size_t words = (size_t)nphases * W * 4, pad = (size_t)2 * W * 4;  // + two NOP phases (prefetch)
+  const size_t words = (size_t)nphases * W * 4, pad = (size_t)vm::PREFETCH * W * 4;  // + NOP phases (prefetch)
   void *dc = nullptr, *di = nullptr, *dout = nullptr;
   HIPCHK(hipMalloc(&dc, (words + pad) * 4));
   c->vm_bufs.push_back(dc);

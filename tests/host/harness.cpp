@@ -97,6 +97,13 @@ int hx_vm_run(const uint32_t* code, uint32_t nphases, uint32_t W, const uint32_t
     for (uint32_t lane = 0; lane < W; ++lane) {
       const uint32_t* w = code + ((size_t)ph * W + lane) * 4;
       ovh::vm::exec(uint4{w[0], w[1], w[2], w[3]}, true, slots, cst, scalar, out);
+      // the interpreter's lazy-reduction invariant: every slot result lies in [0, 2p)
+      const uint32_t op = w[0] & 31, dst = (w[0] >> 5) & 0x7FF;
+      if (op != ovh::vm::OP_NOP && op != ovh::vm::OP_ST) {
+        uint32_t br = 0;
+        for (int k = 0; k < 12; ++k) (void)subc32(slots[dst * 12 + k], ovh::vm::P2_LIMBS[k], br, &br);
+        if (!br) return -1 - (int)ph;
+      }
     }
   return 0;
 }

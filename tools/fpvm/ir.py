@@ -10,7 +10,7 @@ Operations (the interpreter in consensus_overlord_amd/csrc/fpvm.hpp implements e
   lex   z = canonical(a) > (p-1)/2             heavy
   inv   z = a^-1 (0 -> 0)                      heavy+: binary extended Euclid in one lane
   lin   z = ca a + cb b + cc c + cd d          light
-  eq    z = (ca a + cb b) == (cc c + cd d)     light
+  eq    z = a == b                             heavy (from-Montgomery product of a - b)
   sel   z = flag(f) ? y : x                    light
   selb  z = bit k of the unit's scalar ? y : x light
   and/or/xor  on flags                         light
@@ -28,8 +28,8 @@ P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB1
 HALF_P = (P - 1) // 2
 CMAX = 15
 
-HEAVY = {"muls", "sgn0", "lex", "inv", "sop"}
-LIGHT = {"lin", "sel", "eq", "and", "or", "xor", "st", "selb"}
+HEAVY = {"muls", "sgn0", "lex", "inv", "sop", "eq"}
+LIGHT = {"lin", "sel", "and", "or", "xor", "st", "selb"}
 
 
 class Val:
@@ -353,7 +353,7 @@ class Prog:
                 terms = sorted(terms, key=lambda cv: cv[1])
                 op.srcs = tuple([v for _, v in terms] + [None] * (4 - len(terms)))
                 op.coefs = tuple([c for c, _ in terms] + [0] * (4 - len(terms)))
-            elif op.kind in ("muls", "eq"):
+            elif op.kind == "muls":   # eq keeps single operands: the interpreter tests a - b
                 a, b, c, d = op.srcs
                 ca, cb, cc, cd = op.coefs
                 left = try_merge(_norm_terms([(ca, a)] + ([(cb, b)] if b is not None and cb else [])), 2)

@@ -270,7 +270,11 @@ def encode(sc):
                     coefs = tuple(c for c, _ in u)
                     if form[0] == "scaled":
                         scale = form[1]
-            elif k in ("muls", "eq"):
+            elif k == "eq":            # (A - B) * plain 1, flag: zero (fpvm.hpp exec)
+                assert op.coefs == (1, 0, 1, 0) and s[1] is None and s[3] is None, op.coefs
+                A, B, C, D = s[0], s[2], None, None
+                coefs = (1, -1, 1, 0)
+            elif k == "muls":
                 A, B, C, D = s
                 coefs = list(op.coefs)
                 for h in (0, 2):
@@ -303,7 +307,7 @@ def encode(sc):
                 raise ValueError(k)
             dst = sc.slot_of.get(i, 0)
             w0 = OPC[k] | dst << 5 | (op.imm & 63) << 16
-            if k in ("sgn0", "lex"):
+            if k in ("sgn0", "lex", "eq"):
                 cref = sc.consts.ref(1, True)          # plain 1: from-Montgomery product
             elif k == "inv":
                 cref = sc.consts.ref(R_MONT * R_MONT % P, False)   # raw R^3: back to Montgomery
@@ -370,7 +374,7 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
                 elif opc == OPC["lex"]:
                     z = 1 if x > HALF_P else 0
                 elif opc == OPC["eq"]:
-                    z = 1 if x == y else 0
+                    z = 1 if x == 0 else 0
                 else:
                     raise ValueError(opc)
             results.append((dst, z))
