@@ -48,6 +48,8 @@ struct Out {
   uint32_t unit;
 };
 constexpr uint32_t CONST_BASE = 0x800;
+// constant-table entries KTAB + n (n = 0..3) hold n (2p + 1) as raw limbs (tools/fpvm/gen.py)
+constexpr uint32_t KTAB = 1;
 
 VM_FN void ld_slot(Fp& r, const uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
                    uint32_t ref) {
@@ -89,20 +91,43 @@ VM_FN void canon(Fp& r, const Fp& a) {
   for (int j = 0; j < 12; ++j) r.v[j] = br ? a.v[j] : d[j];
 }
 
-// s (13 limbs, s < 2^389) -> r in [0, 2p), r == s mod p. With T = s >> 359 (< 2^30) and
-// Pt = p >> 359, T / (Pt + 1) <= s / p < (T + 1) / Pt, and s / p - T / (Pt + 1) < 3e-4 for
-// s < 248 p; the f32 quotient is shrunk by 2^-20 (three f32 roundings stay below it), so
-// q = floor(f) is floor(s / p) or one less: s - q p lies in [0, 2p).
-VM_FN void reduce2p(Fp& r, const uint32_t* s) {
-  const uint32_t t = (uint32_t)((((uint64_t)s[12] << 32) | s[11]) >> 7);
+// NP = 2^384 - p: adding q NP is subtracting q p modulo 2^384 with a carry chain through
+// 64-bit products (no borrow flags)
+constexpr uint32_t NP_LIMBS[12] = {
+    0u - P_LIMBS[0], ~P_LIMBS[1], ~P_LIMBS[2], ~P_LIMBS[3], ~P_LIMBS[4], ~P_LIMBS[5],
+    ~P_LIMBS[6], ~P_LIMBS[7], ~P_LIMBS[8], ~P_LIMBS[9], ~P_LIMBS[10], ~P_LIMBS[11]};
+static_assert(P_LIMBS[0] != 0, "NP_LIMBS: no borrow out of limb 0");
+
+// f32 quotient estimate floor(x / p) for x = t 2^359 + (lower bits), t = x >> 359 < 2^30: with
+// Pt = p >> 359, t / (Pt + 1) <= x / p < (t + 1) / Pt and x / p - t / (Pt + 1) < 1e-4 for
+// x < 250 p; the quotient is shrunk by 2^-20 (the f32 roundings stay below it), so the result
+// is floor(x / p) or one less.
+VM_FN uint32_t quot_est(uint32_t t) {
   constexpr float QS = (float)((1.0 - 0x1p-20) / (double)((P_LIMBS[11] >> 7) + 1));
-  const uint32_t q = (uint32_t)((float)t * QS);
-  uint64_t pr = 0;
-  uint32_t br = 0;
+  return (uint32_t)((float)t * QS);
+}
+
+// r = k s - q p in [0, 2p) for s < 8p (12 limbs), 1 <= k <= 15: q = quot_est of k s, and
+// k s + q NP modulo 2^384 as one carry chain of 64-bit products.
+VM_FN void scale_reduce(Fp& r, const uint32_t* s, uint32_t k) {
+  const uint32_t q = quot_est(k * (s[11] >> 7));
+  uint64_t acc = 0;
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    pr = (uint64_t)P_LIMBS[j] * q + (pr >> 32);
-    r.v[j] = subc32(s[j], (uint32_t)pr, br, &br);
+    acc = (uint64_t)k * s[j] + (acc >> 32);
+    acc = (uint64_t)q * NP_LIMBS[j] + acc;
+    r.v[j] = (uint32_t)acc;
+  }
+}
+
+// s (13 limbs, s < 250 p < 2^389) -> r in [0, 2p), r == s mod p.
+VM_FN void reduce2p(Fp& r, const uint32_t* s) {
+  const uint32_t q = quot_est((uint32_t)((((uint64_t)s[12] << 32) | s[11]) >> 7));
+  uint64_t acc = 0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    acc = (uint64_t)q * NP_LIMBS[j] + s[j] + (acc >> 32);
+    r.v[j] = (uint32_t)acc;
   }
 }
 
@@ -131,61 +156,67 @@ VM_FN void acc_bias128(uint32_t* acc) {
   acc[12] = prev >> 25;
 }
 
-// d = a + (neg ? 2p - b : b) for two independent (a, b) pairs, carry chains interleaved limb by
-// limb (gfx950 charges wait states for a VALU carry read right after its write).
-VM_FN void add_negsel2(Fp& x, const Fp& A, const Fp& B, bool nx, Fp& y, const Fp& C, const Fp& D, bool ny) {
-  uint32_t nb[12], nd[12], b1 = 0, b2 = 0, c1 = 0, c2 = 0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    nb[j] = subc32(P2_LIMBS[j], B.v[j], b1, &b1);
-    nd[j] = subc32(P2_LIMBS[j], D.v[j], b2, &b2);
-  }
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    x.v[j] = addc32(A.v[j], nx ? nb[j] : B.v[j], c1, &c1);
-    y.v[j] = addc32(C.v[j], ny ? nd[j] : D.v[j], c2, &c2);
-  }
-}
-
-VM_FN void add2(Fp& x, const Fp& A, const Fp& B, Fp& y, const Fp& C, const Fp& D) {
-  uint32_t c1 = 0, c2 = 0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    x.v[j] = addc32(A.v[j], B.v[j], c1, &c1);
-    y.v[j] = addc32(C.v[j], D.v[j], c2, &c2);
-  }
-}
-
 // Product operands x = A + (nx ? 2p - B : B), y = C + (ny ? 2p - D : D) in [0, 4p), no
 // reduction. The negations' borrow chains run only when some lane of the wave has one
-// (`any_neg`); both paths write x, y in full (no register copies at the join).
+// (`any_neg`); both paths write x, y in full (no register copies at the join). The four carry
+// chains are skewed by one limb so no chain reads its carry right after writing it (gfx950
+// wait states).
 VM_FN void pre_add2(Fp& x, const Fp& A, const Fp& B, bool nx, Fp& y, const Fp& C, const Fp& D, bool ny,
                     bool any_neg) {
-  if (any_neg) add_negsel2(x, A, B, nx, y, C, D, ny);
-  else add2(x, A, B, y, C, D);
+  uint32_t c1 = 0, c2 = 0;
+  if (any_neg) {
+    uint32_t nb[12], nd[12], b1 = 0, b2 = 0;
+#pragma unroll
+    for (int j = 0; j < 13; ++j) {
+      if (j < 12) {
+        nb[j] = subc32(P2_LIMBS[j], B.v[j], b1, &b1);
+        nd[j] = subc32(P2_LIMBS[j], D.v[j], b2, &b2);
+      }
+      if (j >= 1) {
+        x.v[j - 1] = addc32(A.v[j - 1], nx ? nb[j - 1] : B.v[j - 1], c1, &c1);
+        y.v[j - 1] = addc32(C.v[j - 1], ny ? nd[j - 1] : D.v[j - 1], c2, &c2);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      x.v[j] = addc32(A.v[j], B.v[j], c1, &c1);
+      y.v[j] = addc32(C.v[j], D.v[j], c2, &c2);
+    }
+  }
 }
 
 // s = A + sb B + sc C + sd D with unit signs (a zero coefficient points its operand at the zero
-// constant): every negated term enters as 2p - X, so s < 8p fits 12 limbs. `any_neg`: some
-// lane of the wave negates a term.
+// constant), s < 8p in 12 limbs: a negated term enters as ~X and the offset K = n (2p + 1)
+// (n negated terms, constant-table entry KTAB + n) turns each ~X into 2p - X modulo 2^384.
+// Four carry chains (A + B', C' + D', their sum, + K) skewed by one limb each.
 VM_FN void lin_sum(uint32_t* s, const Fp& A, const Fp& B, const Fp& C, const Fp& D, int sb, int sc, int sd,
-                   bool any_neg) {
-  Fp u, v;
+                   bool any_neg, const uint32_t* __restrict__ cst) {
+  uint32_t u[12], v[12], w[12], c1 = 0, c2 = 0, c3 = 0, c4 = 0;
   if (any_neg) {
-    // (A + B') and (C' + D') as two chains: C' = 2p - C needs its own borrow chain first
-    uint32_t nc[12], b3 = 0;
+    const uint32_t mb = sb < 0 ? ~0u : 0u, mc = sc < 0 ? ~0u : 0u, md = sd < 0 ? ~0u : 0u;
+    const uint32_t n = (mb & 1u) + (mc & 1u) + (md & 1u);
+    Fp K;
+    ld_slot(K, nullptr, cst, CONST_BASE + KTAB + n);
 #pragma unroll
-    for (int j = 0; j < 12; ++j) nc[j] = subc32(P2_LIMBS[j], C.v[j], b3, &b3);
-    Fp c;
-#pragma unroll
-    for (int j = 0; j < 12; ++j) c.v[j] = sc < 0 ? nc[j] : C.v[j];
-    add_negsel2(u, A, B, sb < 0, v, c, D, sd < 0);
+    for (int j = 0; j < 14; ++j) {
+      if (j < 12) {
+        u[j] = addc32(A.v[j], B.v[j] ^ mb, c1, &c1);
+        v[j] = addc32(C.v[j] ^ mc, D.v[j] ^ md, c2, &c2);
+      }
+      if (j >= 1 && j <= 12) w[j - 1] = addc32(u[j - 1], v[j - 1], c3, &c3);
+      if (j >= 2) s[j - 2] = addc32(w[j - 2], K.v[j - 2], c4, &c4);
+    }
   } else {
-    add2(u, A, B, v, C, D);
-  }
-  uint32_t c3 = 0;
 #pragma unroll
-  for (int j = 0; j < 12; ++j) s[j] = addc32(u.v[j], v.v[j], c3, &c3);
+    for (int j = 0; j < 13; ++j) {
+      if (j < 12) {
+        u[j] = addc32(A.v[j], B.v[j], c1, &c1);
+        v[j] = addc32(C.v[j], D.v[j], c2, &c2);
+      }
+      if (j >= 1) s[j - 1] = addc32(u[j - 1], v[j - 1], c3, &c3);
+    }
+  }
   s[12] = 0;
 }
 
@@ -296,20 +327,11 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
   }
   if (wave_any(is_lin)) {
     uint32_t s[13];
-    lin_sum(s, A, B, C, D, cb, cc, cd, wave_any(is_lin && (cb < 0 || cc < 0 || cd < 0)));
+    lin_sum(s, A, B, C, D, cb, cc, cd, wave_any(is_lin && (cb < 0 || cc < 0 || cd < 0)), cst);
+    // "scaled" form k * (unit sum), k < 16 (k <= 1: unchanged)
     const uint32_t k = (in.w >> 20) & 15;
-    if (wave_any(is_lin && k > 1)) {  // "scaled" form: k * (unit sum), k < 16 (k <= 1: unchanged)
-      const uint32_t kk = k > 1 ? k : 1u;
-      uint64_t pr = 0;
-#pragma unroll
-      for (int j = 0; j < 12; ++j) {
-        pr = (uint64_t)s[j] * kk + (pr >> 32);
-        s[j] = (uint32_t)pr;
-      }
-      s[12] = (uint32_t)(pr >> 32);
-    }
     Fp l;
-    reduce2p(l, s);
+    scale_reduce(l, s, k > 1 ? k : 1u);
     if (is_lin) st_slot(slots, dst, l);
   }
   const bool rare = op != OP_NOP && !is_mul && !is_lin;

@@ -37,6 +37,7 @@
 #include "keygen.hpp"
 #include "sm3.hpp"
 #include "vm_progs.inc"
+static_assert(VM_KTAB == ovh::vm::KTAB, "lin offset table (tools/fpvm/gen.py KTAB)");
 
 using namespace ovh;
 

@@ -27,6 +27,7 @@ import math
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 HALF_P = (P - 1) // 2
 CMAX = 15
+LIN_WIDTH = 4   # operands of a lin op (the interpreter's widest linear combination)
 
 HEAVY = {"muls", "sgn0", "lex", "inv", "sop", "eq"}
 LIGHT = {"lin", "sel", "and", "or", "xor", "st", "selb"}
@@ -94,11 +95,12 @@ def _expand_unit(terms, width):
     return ex if len(ex) <= width else None
 
 
-def lin_form(terms, width=4):
+def lin_form(terms, width=None):
     """How the interpreter evaluates sum c_i v_i (fpvm.hpp exec):
     ("unit", u)      u = <= width unit terms, plain modular adds / subs;
     ("scaled", k, u) k * (unit sum), 2 <= k <= 15: one small-scalar product + reduction;
     ("acc", terms)   general signed 13-limb accumulation + reduction (slow)."""
+    width = LIN_WIDTH if width is None else width
     terms = [(c, v) for c, v in terms if c]
     u = _expand_unit(terms, width)
     if u is not None:
@@ -195,7 +197,7 @@ class Prog:
             return Val(self, t[0][1])
         out = None
         while t:
-            n = 4 if out is None else 3
+            n = LIN_WIDTH if out is None else LIN_WIDTH - 1
             chunk, t = t[:n], t[n:]
             if out is not None:
                 chunk = [(1, out.id)] + chunk
@@ -206,8 +208,8 @@ class Prog:
                     c = 1 if c > 0 else -1
                 fixed.append((c, v))
             chunk = sorted(fixed, key=lambda cv: cv[1])
-            srcs = [v for _, v in chunk] + [None] * (4 - len(chunk))
-            coefs = [c for c, _ in chunk] + [0] * (4 - len(chunk))
+            srcs = [v for _, v in chunk] + [None] * (LIN_WIDTH - len(chunk))
+            coefs = [c for c, _ in chunk] + [0] * (LIN_WIDTH - len(chunk))
             out = self._op("lin", srcs, coefs)
         return out
 
@@ -319,7 +321,7 @@ class Prog:
 
         def cost(terms, limit):
             f = lin_form(terms, limit)[0]
-            return FORM_COST[f] if limit == 4 else (0 if f == "unit" else 1000)  # muls operands: unit only
+            return FORM_COST[f] if limit == LIN_WIDTH else (0 if f == "unit" else 1000)  # muls operands: unit only
 
         def fusable(j):
             return j is not None and self.ops[j].kind == "lin" and j not in outs and (uses[j] == 1 or dup)
@@ -335,7 +337,7 @@ class Prog:
                         cand = _norm_terms(terms[:k] + terms[k + 1:] + sub)
                         # a single-use producer disappears (its cost is credited); a shared one
                         # is duplicated into this consumer only if the consumer gets no dearer
-                        credit = cost(self._lin_terms(self.ops[v]), 4) if uses[v] == 1 else 0
+                        credit = cost(self._lin_terms(self.ops[v]), LIN_WIDTH) if uses[v] == 1 else 0
                         if len(cand) <= limit and all(abs(c3) <= CMAX for c3, _ in cand) and \
                                 cost(cand, limit) <= cost(terms, limit) + credit:
                             uses[v] -= 1
@@ -349,10 +351,10 @@ class Prog:
         for i in sorted(live):
             op = self.ops[i]
             if op.kind == "lin":
-                terms = try_merge(self._lin_terms(op), 4)
+                terms = try_merge(self._lin_terms(op), LIN_WIDTH)
                 terms = sorted(terms, key=lambda cv: cv[1])
-                op.srcs = tuple([v for _, v in terms] + [None] * (4 - len(terms)))
-                op.coefs = tuple([c for c, _ in terms] + [0] * (4 - len(terms)))
+                op.srcs = tuple([v for _, v in terms] + [None] * (LIN_WIDTH - len(terms)))
+                op.coefs = tuple([c for c, _ in terms] + [0] * (LIN_WIDTH - len(terms)))
             elif op.kind == "muls":   # eq keeps single operands: the interpreter tests a - b
                 a, b, c, d = op.srcs
                 ca, cb, cc, cd = op.coefs

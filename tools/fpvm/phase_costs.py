@@ -30,27 +30,25 @@ def lane_paths(w):
     if k == "nop":
         return set()
     if k in ("st", "selb", "sel", "inv"):
-        return {k}
+        return {"rare", k}
     if k in ("and", "or", "xor"):
-        return {"logic"}
+        return {"rare", "logic"}
     ca, cb, cc, cd = (_s5((w[3] >> (5 * q)) & 31) for q in range(4))
     if k == "lin":
         unit = ca == 1 and all(-1 <= x <= 1 for x in (cb, cc, cd))
         if not unit:
-            return {"lin_acc"}
-        p = {"lin_unit"}
-        if cc:
-            p.add("lin_y")
+            return {"rare", "lin_acc"}
+        p = {"lin"}
+        if cb < 0 or cc < 0 or cd < 0:
+            p.add("lin_neg")
         if (w[3] >> 20) & 15 > 1:
             p.add("lin_scale")
         return p
-    p = {"mulclass"}
-    for side, (a, b) in (("x", (ca, cb)), ("y", (cc, cd))):
-        if a == 1 and -1 <= b <= 1:
-            p.add("%s_%s" % (side, {0: "copy", 1: "add", -1: "sub"}[b]))
-        else:
-            p.add("%s_acc" % side)
-    p.add({"muls": "fpmul", "sgn0": "fpmul", "lex": "fpmul", "eq": "eq"}[k])
+    p = {"mul"}
+    if cb < 0 or cd < 0:
+        p.add("mul_neg")
+    if k != "muls":
+        p.add("flag")
     return p
 
 
