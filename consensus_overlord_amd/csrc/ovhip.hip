@@ -750,6 +750,7 @@ struct ovh_ctx {
   // run on fstream while batch k + 1's per-vote stages run on stream; OVH_BATCH_SLOTS slots of
   // batch state rotate (a slot is reused only after its final-stream work finished).
   hipStream_t fstream = nullptr;
+  hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of each slot (all == fstream, see ovh_create)
   hipStream_t hstream = nullptr;  // hash_to_field of the next batch, beside the current vote
   hipEvent_t ev_h[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
@@ -1109,12 +1110,13 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
   int reg = 1;
   CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 64));
   HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
-  HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_front[slot], 0));
-  CHK(fold_down(c, slot, c->fstream, 1, &reg, &m, 4));
+  hipStream_t fst = c->fs[slot];
+  HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
+  CHK(fold_down(c, slot, fst, 1, &reg, &m, 4));
   int32_t* verdict = c->result + RES_BATCH + slot;
-  enqueue_final(c, c->fstream, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict);
-  enqueue_bisect(c, c->fstream, slot, (uint32_t)n, d_codes, verdict);
-  HIPCHK(hipEventRecord(c->ev_back[slot], c->fstream));
+  enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict);
+  enqueue_bisect(c, fst, slot, (uint32_t)n, d_codes, verdict);
+  HIPCHK(hipEventRecord(c->ev_back[slot], fst));
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1334,10 +1336,14 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   bool ok = xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
+            (c->fs[0] = c->fstream) != nullptr &&
             hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->part_out, 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
             hipMemset(c->result, 0, 64) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
+  // one final stream: two finals in flight would each take a SIMD beside a vote wave and LDS a
+  // vote workgroup needs (measured r02g: the vote kernel slowed from 4.6 to 5.3 ms)
+  for (int k = 1; ok && k < OVH_BATCH_SLOTS; ++k) c->fs[k] = c->fstream;
   for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k)
     ok = hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_h[k], hipEventDisableTiming) == hipSuccess &&
@@ -1385,8 +1391,9 @@ ovh_ctx* ovh_create_multi(const int* devices, int ndev, const uint8_t* dst, size
 
 static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
-  for (hipStream_t s : {c->stream, c->fstream, c->hstream})
+  for (hipStream_t s : {c->stream, c->hstream})
     if (s) (void)hipStreamSynchronize(s);
+  if (c->fstream) (void)hipStreamSynchronize(c->fstream);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k]})
       if (p) (void)hipFree(p);
@@ -1404,8 +1411,9 @@ static void destroy_one(ovh_ctx* c) {
     if (c->ev0[k]) (void)hipEventDestroy(c->ev0[k]);
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
   }
-  for (hipStream_t s : {c->stream, c->fstream, c->hstream})
+  for (hipStream_t s : {c->stream, c->hstream})
     if (s) (void)hipStreamDestroy(s);
+  if (c->fstream) (void)hipStreamDestroy(c->fstream);
   delete c;
 }
 
@@ -2039,23 +2047,23 @@ int ovh_combine_partials_device_async(ovh_ctx* c, size_t k, const uint8_t* d_par
   HIPCHK(hipSetDevice(c->device));
   if (n != c->last_n || (n && c->slot_n[c->last_slot] != n)) return OVH_ERR_ARG;
   const int slot = c->last_slot;
-  hipStream_t st = (hipStream_t)stream;
+  hipStream_t st = (hipStream_t)stream, fst = c->fs[slot];
   if (st) {  // the partials are complete in `st` order (after the caller's all-gather)
     HIPCHK(hipEventRecord(c->ev_x[2], st));
-    HIPCHK(hipStreamWaitEvent(c->fstream, c->ev_x[2], 0));
+    HIPCHK(hipStreamWaitEvent(fst, c->ev_x[2], 0));
   }
   uint32_t* scratch = c->fin + (size_t)slot * FIN_STRIDE;
   Slab F, S;
   uint32_t m;
-  CHK(stage_partials(c, c->fstream, k, d_partials, scratch, &F, &S, &m));
+  CHK(stage_partials(c, fst, k, d_partials, scratch, &F, &S, &m));
   if (st) {  // the caller may reuse d_partials once they were read
-    HIPCHK(hipEventRecord(c->ev_x[3], c->fstream));
+    HIPCHK(hipEventRecord(c->ev_x[3], fst));
     HIPCHK(hipStreamWaitEvent(st, c->ev_x[3], 0));
   }
   int32_t* verdict = c->result + RES_COMBINE + slot;
-  enqueue_final(c, c->fstream, F, S, m, verdict);
-  if (n) enqueue_bisect(c, c->fstream, slot, (uint32_t)n, d_codes, verdict);
-  HIPCHK(hipEventRecord(c->ev_back[slot], c->fstream));
+  enqueue_final(c, fst, F, S, m, verdict);
+  if (n) enqueue_bisect(c, fst, slot, (uint32_t)n, d_codes, verdict);
+  HIPCHK(hipEventRecord(c->ev_back[slot], fst));
   HIPCHK(hipGetLastError());
   return 0;
 }
