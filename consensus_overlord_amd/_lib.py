@@ -6,7 +6,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libovhip.so")
+# OVH_LIBPATH: an alternative build of the same library (diagnostic A/B runs only)
+LIB_PATH = os.environ.get("OVH_LIBPATH") or os.path.join(_HERE, "libovhip.so")
 
 _u8p = ctypes.c_char_p
 _sz = ctypes.c_size_t

@@ -329,8 +329,12 @@ __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const ui
 }
 
 // Final: prod F * Miller(-G1, sum S) over in[0..m-1] (m <= 4) -> FE == 1 -> *result.
+#ifndef OVH_FINAL_PRIO
+#define OVH_FINAL_PRIO 0
+#endif
 __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
                                                  Slab inS, int32_t* __restrict__ result) {
+  if (OVH_FINAL_PRIO) __builtin_amdgcn_s_setprio(OVH_FINAL_PRIO);
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -1015,18 +1019,8 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   uint64_t seed, base;
   CHK(draw_seed(c, &seed, &base));
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
-  if (pipelined) {
-    // hash_to_field on its own stream, as soon as the slot's previous batch has finished its
-    // per-vote stages (the only reader of the S_U planes), so it runs beside the current vote
-    // kernel; the vote waits for it
-    HIPCHK(hipStreamWaitEvent(c->hstream, c->ev_front[slot], 0));
-    {
-      StageScope p(c, ST_H2F, c->hstream);
-      k_h2f<<<nblk(n), WG, 0, c->hstream>>>(n, d_hashes, c->xmd, s);
-    }
-    HIPCHK(hipEventRecord(c->ev_h[slot], c->hstream));
-    HIPCHK(hipStreamWaitEvent(st, c->ev_h[slot], 0));
-  } else {
+  {  // hash_to_field right before the vote kernel on the same stream (a cross-stream event
+     // hand-off cost more than the kernel, r02f/r02g kernel traces)
     StageScope p(c, ST_H2F);
     k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s);
   }
@@ -1039,7 +1033,7 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
       k_vm_vote_t<<<nwg, 64, LDS_VOTE_T, st>>>(n, c->vm_vote_t, c->vm_fold, c->vm_consts, key.pts, d_sigs, s, seed,
                                                base, d_codes, region_F(c, slot, 0));
   }
-  {
+  {  // fold level 1: R0 -> R1 (one partial per 16-vote group, kept for the bisection)
     StageScope p(c, ST_FOLD);
     const uint32_t m1 = (nwg + 3) / 4;
     k_vm_fold<VM_FOLD_UNITS><<<(m1 + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(
@@ -1341,8 +1335,9 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
             hipMalloc(&c->part_out, 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
             hipMemset(c->result, 0, 64) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
-  // one final stream: two finals in flight would each take a SIMD beside a vote wave and LDS a
-  // vote workgroup needs (measured r02g: the vote kernel slowed from 4.6 to 5.3 ms)
+  // one final stream for all slots: a final shares a SIMD with a vote wave and runs at half
+  // speed there; with two in flight (3 slots, a stream each: r02i) every third vote kernel lost
+  // 2.4 ms to a workgroup that found no LDS beside two finals and a fold
   for (int k = 1; ok && k < OVH_BATCH_SLOTS; ++k) c->fs[k] = c->fstream;
   for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k)
     ok = hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) == hipSuccess &&
