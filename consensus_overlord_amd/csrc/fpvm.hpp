@@ -107,10 +107,10 @@ VM_FN uint32_t quot_est(uint32_t t) {
   return (uint32_t)((float)t * QS);
 }
 
-// r = k s - q p in [0, 2p) for s < 8p (12 limbs), 1 <= k <= 15: q = quot_est of k s, and
+// r = k s - q p in [0, 2p) for s < 16p (13 limbs), 1 <= k <= 15: q = quot_est of k s, and
 // k s + q NP modulo 2^384 as one carry chain of 64-bit products.
 VM_FN void scale_reduce(Fp& r, const uint32_t* s, uint32_t k) {
-  const uint32_t q = quot_est(k * (s[11] >> 7));
+  const uint32_t q = quot_est(k * (uint32_t)((((uint64_t)s[12] << 32) | s[11]) >> 7));
   uint64_t acc = 0;
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
@@ -145,15 +145,15 @@ VM_FN void acc_term(uint32_t* acc, const Fp& X, int c) {
   acc[12] = acc[12] + ((uint32_t)(pr >> 32) ^ mask) + cy;
 }
 
-// acc = 128 p (13 limbs): the bias that keeps a signed sum of four |c| <= 15 terms >= 0
-VM_FN void acc_bias128(uint32_t* acc) {
+// acc = 256 p (13 limbs): the bias that keeps a signed sum of eight |c| <= 15 terms >= 0
+VM_FN void acc_bias256(uint32_t* acc) {
   uint32_t prev = 0;
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    acc[j] = (P_LIMBS[j] << 7) | (prev >> 25);
+    acc[j] = (P_LIMBS[j] << 8) | (prev >> 24);
     prev = P_LIMBS[j];
   }
-  acc[12] = prev >> 25;
+  acc[12] = prev >> 24;
 }
 
 // Product operands x = A + (nx ? 2p - B : B), y = C + (ny ? 2p - D : D) in [0, 4p), no
@@ -186,22 +186,22 @@ VM_FN void pre_add2(Fp& x, const Fp& A, const Fp& B, bool nx, Fp& y, const Fp& C
   }
 }
 
-// s = A + sb B + sc C + sd D with unit signs (a zero coefficient points its operand at the zero
-// constant), s < 8p in 12 limbs: a negated term enters as ~X and the offset K = n (2p + 1)
+// s = sa A + sb B + sc C + sd D with unit signs (a zero coefficient points its operand at the
+// zero constant), s < 8p in 12 limbs: a negated term enters as ~X and the offset K = n (2p + 1)
 // (n negated terms, constant-table entry KTAB + n) turns each ~X into 2p - X modulo 2^384.
-// Four carry chains (A + B', C' + D', their sum, + K) skewed by one limb each.
-VM_FN void lin_sum(uint32_t* s, const Fp& A, const Fp& B, const Fp& C, const Fp& D, int sb, int sc, int sd,
-                   bool any_neg, const uint32_t* __restrict__ cst) {
+// Four carry chains (A' + B', C' + D', their sum, + K) skewed by one limb each.
+VM_FN void lin_sum(uint32_t* s, const Fp& A, const Fp& B, const Fp& C, const Fp& D, int sa, int sb, int sc,
+                   int sd, bool any_neg, const uint32_t* __restrict__ cst) {
   uint32_t u[12], v[12], w[12], c1 = 0, c2 = 0, c3 = 0, c4 = 0;
   if (any_neg) {
-    const uint32_t mb = sb < 0 ? ~0u : 0u, mc = sc < 0 ? ~0u : 0u, md = sd < 0 ? ~0u : 0u;
-    const uint32_t n = (mb & 1u) + (mc & 1u) + (md & 1u);
+    const uint32_t ma = sa < 0 ? ~0u : 0u, mb = sb < 0 ? ~0u : 0u, mc = sc < 0 ? ~0u : 0u, md = sd < 0 ? ~0u : 0u;
+    const uint32_t n = (ma & 1u) + (mb & 1u) + (mc & 1u) + (md & 1u);
     Fp K;
     ld_slot(K, nullptr, cst, CONST_BASE + KTAB + n);
 #pragma unroll
     for (int j = 0; j < 14; ++j) {
       if (j < 12) {
-        u[j] = addc32(A.v[j], B.v[j] ^ mb, c1, &c1);
+        u[j] = addc32(A.v[j] ^ ma, B.v[j] ^ mb, c1, &c1);
         v[j] = addc32(C.v[j] ^ mc, D.v[j] ^ md, c2, &c2);
       }
       if (j >= 1 && j <= 12) w[j - 1] = addc32(u[j - 1], v[j - 1], c3, &c3);
@@ -286,15 +286,22 @@ extern bool g_host_any;
 inline bool wave_any(bool p) { return p || g_host_any; }
 #endif
 
-// One phase of one lane. `in` = (w0, A|B<<16, C|D<<16, coefficients). The common ops run behind
-// wave-uniform branches (a block runs when any lane of the wave needs it) and each lane stores
-// the result of its own op:
+// w0 flag of a wide-program lin op that uses operands E..H (tools/fpvm/sched.py WIDE_FLAG)
+constexpr uint32_t WIDE_FLAG = 1u << 22;
+
+// One phase of one lane. `in` = (w0, A|B<<16, C|D<<16, coefficients of A..D); programs with
+// NW = 8 words per lane also pass `in2` = (E|F<<16, G|H<<16, coefficients of E..H, 0), the
+// operands of up to eight-term linear combinations. The common ops run behind wave-uniform
+// branches (a block runs when any lane of the wave needs it) and each lane stores the result of
+// its own op:
 //   products  x = A + cb B, y = C + cd D (unit signs), m = x y: muls; sgn0 / lex / eq take the
 //             from-Montgomery product (y = plain 1; eq: x = A - B) and flag its canonical value;
-//   lin       k (A + cb B + cc C + cd D), unit signs, 1 <= k <= 15;
+//   lin       k (A + cb B + cc C + cd D [+ ce E + ... + ch H]), unit signs, 1 <= k <= 15;
 //   rare      sel, selb, logic, st, inv, lin with general coefficients (per-lane branches).
-VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
-                uint64_t scalar, const Out& out) {
+template <int NW>
+VM_FN void exec(const uint4 in, const uint4 in2, bool active, uint32_t* __restrict__ slots,
+                const uint32_t* __restrict__ cst, uint64_t scalar, const Out& out) {
+  static_assert(NW == 4 || NW == 8, "instruction words per lane");
   const uint32_t op = active ? (in.x & 31) : (uint32_t)OP_NOP;
   if (!wave_any(op != OP_NOP)) return;
   const uint32_t dst = (in.x >> 5) & 0x7FF;
@@ -307,8 +314,12 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
   ld_slot(D, slots, cst, in.z >> 16);
   const int ca = ((int)(in.w << 27)) >> 27, cb = ((int)(in.w << 22)) >> 27;
   const int cc = ((int)(in.w << 17)) >> 27, cd = ((int)(in.w << 12)) >> 27;
+  const bool wide = NW == 8 && (in.x & WIDE_FLAG) != 0;
+  const int ce = NW == 8 ? ((int)(in2.z << 27)) >> 27 : 0, cf = NW == 8 ? ((int)(in2.z << 22)) >> 27 : 0;
+  const int cg = NW == 8 ? ((int)(in2.z << 17)) >> 27 : 0, ch = NW == 8 ? ((int)(in2.z << 12)) >> 27 : 0;
   const bool is_mul = op == OP_MULS || op == OP_SGN0 || op == OP_LEX || op == OP_EQ;
-  const bool lin_unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1;
+  const bool lin_unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1 &&
+                        ce >= -1 && ce <= 1 && cf >= -1 && cf <= 1 && cg >= -1 && cg <= 1 && ch >= -1 && ch <= 1;
   const bool is_lin = op == OP_LIN && lin_unit;
   if (wave_any(is_mul)) {
     Fp x, y, m;
@@ -327,7 +338,19 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
   }
   if (wave_any(is_lin)) {
     uint32_t s[13];
-    lin_sum(s, A, B, C, D, cb, cc, cd, wave_any(is_lin && (cb < 0 || cc < 0 || cd < 0)), cst);
+    lin_sum(s, A, B, C, D, 1, cb, cc, cd, wave_any(is_lin && (cb < 0 || cc < 0 || cd < 0)), cst);
+    if (NW == 8 && wave_any(is_lin && wide)) {  // second group E..H (all four signed): s < 16p
+      Fp E, F, G, H;
+      ld_slot(E, slots, cst, in2.x & 0xFFFF);
+      ld_slot(F, slots, cst, in2.x >> 16);
+      ld_slot(G, slots, cst, in2.y & 0xFFFF);
+      ld_slot(H, slots, cst, in2.y >> 16);
+      uint32_t s2[13], c = 0;
+      lin_sum(s2, E, F, G, H, ce, cf, cg, ch, wave_any(is_lin && (ce < 0 || cf < 0 || cg < 0 || ch < 0)), cst);
+#pragma unroll
+      for (int j = 0; j < 12; ++j) s[j] = addc32(s[j], s2[j], c, &c);
+      s[12] = c;
+    }
     // "scaled" form k * (unit sum), k < 16 (k <= 1: unchanged)
     const uint32_t k = (in.w >> 20) & 15;
     Fp l;
@@ -356,41 +379,68 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
 #endif
     } else if (op == OP_LIN) {  // general coefficients
       uint32_t acc[13];
-      acc_bias128(acc);
+      acc_bias256(acc);
       acc_term(acc, A, ca);
       acc_term(acc, B, cb);
       acc_term(acc, C, cc);
       acc_term(acc, D, cd);
+      if (NW == 8 && wide) {
+        Fp E;
+        ld_slot(E, slots, cst, in2.x & 0xFFFF);
+        acc_term(acc, E, ce);
+        ld_slot(E, slots, cst, in2.x >> 16);
+        acc_term(acc, E, cf);
+        ld_slot(E, slots, cst, in2.y & 0xFFFF);
+        acc_term(acc, E, cg);
+        ld_slot(E, slots, cst, in2.y >> 16);
+        acc_term(acc, E, ch);
+      }
       reduce2p(z, acc);
     }
     if (rare && op != OP_ST) st_slot(slots, dst, z);
   }
 }
 
-// Run `nphases` phases of a W-lane program. Every lane of the workgroup must call this; lanes
-// of inactive slices pass active = false. The VM kernels are single-wave workgroups, so no
-// phase barrier is needed: a wave's LDS operations are performed in issue order, and a slot a
-// phase writes is read from the next phase on (tools/fpvm/sched.py), so the next phase's loads
-// may issue while this phase's stores are still in flight.
+// Run `nphases` phases of a W-lane program with NW instruction words per lane (the code is
+// phase-major: lane l of phase t at uint4 index (t W + l) NW / 4). Every lane of the workgroup
+// must call this; lanes of inactive slices pass active = false. The VM kernels are single-wave
+// workgroups, so no phase barrier is needed: a wave's LDS operations are performed in issue
+// order, and a slot a phase writes is read from the next phase on (tools/fpvm/sched.py), so the
+// next phase's loads may issue while this phase's stores are still in flight.
 #if defined(__HIPCC__)
+template <int NW>
 __device__ __forceinline__ void run(const uint4* __restrict__ code, uint32_t nphases, uint32_t W, uint32_t lane,
                                     bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
                                     uint64_t scalar, const Out& out, uint64_t* __restrict__ trace = nullptr) {
   static_assert(PREFETCH == 4, "prefetch ring below is 4 deep");
+  constexpr uint32_t Q = NW / 4;  // uint4 per lane per phase
   // trace (diagnostics, OVH_FLAG_VM_TRACE): wall clock after every phase
   if (trace && threadIdx.x == 0) trace[0] = wall_clock64();
   // instructions are prefetched PREFETCH phases ahead (an HBM / L2 round trip outlasts a light
   // phase); the code carries PREFETCH trailing NOP phases
-  uint4 q0 = code[lane], q1 = code[(size_t)W + lane], q2 = code[(size_t)2 * W + lane],
-        q3 = code[(size_t)3 * W + lane];
+  auto at = [&](uint32_t ph, uint32_t k) { return code[((size_t)ph * W + lane) * Q + k]; };
+  uint4 q0 = at(0, 0), q1 = at(1, 0), q2 = at(2, 0), q3 = at(3, 0);
+  uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
+  if (Q == 2) {
+    r0 = at(0, 1);
+    r1 = at(1, 1);
+    r2 = at(2, 1);
+    r3 = at(3, 1);
+  }
 #pragma unroll 1
   for (uint32_t ph = 0; ph < nphases; ++ph) {
-    const uint4 cur = q0;
+    const uint4 cur = q0, cur2 = r0;
     q0 = q1;
     q1 = q2;
     q2 = q3;
-    q3 = code[(size_t)(ph + PREFETCH) * W + lane];
-    exec(cur, active, slots, cst, scalar, out);
+    q3 = at(ph + PREFETCH, 0);
+    if (Q == 2) {
+      r0 = r1;
+      r1 = r2;
+      r2 = r3;
+      r3 = at(ph + PREFETCH, 1);
+    }
+    exec<NW>(cur, cur2, active, slots, cst, scalar, out);
     if (trace) {
       __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (threadIdx.x == 0) trace[ph + 1] = wall_clock64();

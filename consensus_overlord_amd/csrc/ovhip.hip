@@ -221,7 +221,7 @@ __device__ __forceinline__ void fold_unit(uint32_t t, uint32_t m, const VmDev& p
     }
   }
   __syncthreads();
-  vm::run(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  vm::run<VM_FOLD_NW>(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
   if (active) {
     for (uint32_t k = lane; k < PART_PLANES; k += VM_FOLD_W) {
       Fp v;
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
     }
   }
   __syncthreads();
-  vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
+  vm::run<VM_VOTE_NW>(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
           vm::Out{s.p, s.cap, i},
           blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) {
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const u
     slot_put(slots, VM_FINAL_IN[k], v.v);
   }
   __syncthreads();
-  vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0},
+  vm::run<VM_FINAL_NW>(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0},
           blockIdx.x == 0 ? prog.trace : nullptr);
   if (lane == 0) *result = slot_flag_get(slots, VM_FINAL_OUT[0]) ? 1 : 0;
 }
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
     }
   }
   __syncthreads();
-  vm::run(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
+  vm::run<VM_VOTE_T_NW>(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
           vm::Out{s.p, s.cap, i}, blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) {
     const uint32_t sf = hdr[0], pf = hdr[1];
@@ -459,7 +459,7 @@ __device__ __forceinline__ bool final_one(uint32_t u, const VmDev& prog, const u
     slot_put(slots, VM_FINAL_IN[k], v.v);
   }
   __syncthreads();
-  vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  vm::run<VM_FINAL_NW>(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
   return slot_flag_get(slots, VM_FINAL_OUT[0]) != 0;
 }
 
@@ -825,9 +825,10 @@ static_assert(VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_NSLOTS * 12 + 4) &&
                   VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_T_NSLOTS * 12 + 4),
               "fused fold reuses the vote slots");
 
-static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphases, uint32_t W, const uint16_t* in,
-                     uint32_t nin, const uint16_t* out, uint32_t nout) {
-  const size_t words = (size_t)nphases * W * 4, pad = (size_t)vm::PREFETCH * W * 4;  // + NOP phases (prefetch)
+static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphases, uint32_t W, uint32_t NW,
+                     const uint16_t* in, uint32_t nin, const uint16_t* out, uint32_t nout) {
+  // + PREFETCH trailing NOP phases (instruction prefetch)
+  const size_t words = (size_t)nphases * W * NW, pad = (size_t)vm::PREFETCH * W * NW;
   void *dc = nullptr, *di = nullptr, *dout = nullptr;
   HIPCHK(hipMalloc(&dc, (words + pad) * 4));
   c->vm_bufs.push_back(dc);
@@ -857,13 +858,13 @@ static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphase
 static int vm_init(ovh_ctx* c) {
   HIPCHK(hipMalloc(&c->vm_consts, sizeof(VM_CONST_WORDS)));
   HIPCHK(hipMemcpy(c->vm_consts, VM_CONST_WORDS, sizeof(VM_CONST_WORDS), hipMemcpyHostToDevice));
-  CHK(vm_upload(c, c->vm_vote, VM_VOTE_CODE, VM_VOTE_NPHASES, VM_VOTE_W, VM_VOTE_IN, VM_VOTE_NIN, VM_VOTE_OUT,
+  CHK(vm_upload(c, c->vm_vote, VM_VOTE_CODE, VM_VOTE_NPHASES, VM_VOTE_W, VM_VOTE_NW, VM_VOTE_IN, VM_VOTE_NIN, VM_VOTE_OUT,
                 VM_VOTE_NOUT));
-  CHK(vm_upload(c, c->vm_vote_t, VM_VOTE_T_CODE, VM_VOTE_T_NPHASES, VM_VOTE_T_W, VM_VOTE_T_IN, VM_VOTE_T_NIN,
+  CHK(vm_upload(c, c->vm_vote_t, VM_VOTE_T_CODE, VM_VOTE_T_NPHASES, VM_VOTE_T_W, VM_VOTE_T_NW, VM_VOTE_T_IN, VM_VOTE_T_NIN,
                 VM_VOTE_T_OUT, VM_VOTE_T_NOUT));
-  CHK(vm_upload(c, c->vm_fold, VM_FOLD_CODE, VM_FOLD_NPHASES, VM_FOLD_W, VM_FOLD_IN, VM_FOLD_NIN, VM_FOLD_OUT,
+  CHK(vm_upload(c, c->vm_fold, VM_FOLD_CODE, VM_FOLD_NPHASES, VM_FOLD_W, VM_FOLD_NW, VM_FOLD_IN, VM_FOLD_NIN, VM_FOLD_OUT,
                 VM_FOLD_NOUT));
-  CHK(vm_upload(c, c->vm_final, VM_FINAL_CODE, VM_FINAL_NPHASES, VM_FINAL_W, VM_FINAL_IN, VM_FINAL_NIN, VM_FINAL_OUT,
+  CHK(vm_upload(c, c->vm_final, VM_FINAL_CODE, VM_FINAL_NPHASES, VM_FINAL_W, VM_FINAL_NW, VM_FINAL_IN, VM_FINAL_NIN, VM_FINAL_OUT,
                 VM_FINAL_NOUT));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote_t, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE_T));

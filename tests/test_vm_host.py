@@ -50,9 +50,9 @@ def run_vm(hx, consts, sc, words, inputs, scalar, any_all):
     cst = np.asarray(consts.words(), dtype=np.uint32).ravel()
     planes = np.zeros(64 * 12, dtype=np.uint32)
     u32p = ctypes.POINTER(ctypes.c_uint32)
-    hx.hx_vm_run.argtypes = [u32p, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, ctypes.c_uint64, u32p,
-                             ctypes.c_uint32, ctypes.c_int]
-    assert hx.hx_vm_run(code.ctypes.data_as(u32p), sc.nrounds, sc.W, cst.ctypes.data_as(u32p),
+    hx.hx_vm_run.argtypes = [u32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, ctypes.c_uint64,
+                             u32p, ctypes.c_uint32, ctypes.c_int]
+    assert hx.hx_vm_run(code.ctypes.data_as(u32p), sc.nrounds, sc.W, sched.words_per_lane(prog), cst.ctypes.data_as(u32p),
                         slots.ctypes.data_as(u32p), scalar, planes.ctypes.data_as(u32p), 64, any_all) == 0
     out = {}
     for name, v in prog.outputs.items():

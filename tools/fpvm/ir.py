@@ -27,7 +27,7 @@ import math
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 HALF_P = (P - 1) // 2
 CMAX = 15
-LIN_WIDTH = 4   # operands of a lin op (the interpreter's widest linear combination)
+LIN_WIDTH = 4   # default operands of a lin op (Prog.lin_width: 4, or 8 for wide-instruction programs)
 
 HEAVY = {"muls", "sgn0", "lex", "inv", "sop", "eq"}
 LIGHT = {"lin", "sel", "and", "or", "xor", "st", "selb"}
@@ -121,8 +121,9 @@ FORM_COST = {"unit": 1, "scaled": 2, "acc": 6}
 class Prog:
     """A traced program. ops[i] defines value i. kind 'in' = input, 'const' = constant."""
 
-    def __init__(self, name):
+    def __init__(self, name, lin_width: int = LIN_WIDTH):
         self.name = name
+        self.lin_width = lin_width   # operands of a lin op (8: the 32-byte instruction format)
         self.ops = []
         self.outputs = {}
         self.inputs = {}
@@ -197,7 +198,7 @@ class Prog:
             return Val(self, t[0][1])
         out = None
         while t:
-            n = LIN_WIDTH if out is None else LIN_WIDTH - 1
+            n = self.lin_width if out is None else self.lin_width - 1
             chunk, t = t[:n], t[n:]
             if out is not None:
                 chunk = [(1, out.id)] + chunk
@@ -208,8 +209,8 @@ class Prog:
                     c = 1 if c > 0 else -1
                 fixed.append((c, v))
             chunk = sorted(fixed, key=lambda cv: cv[1])
-            srcs = [v for _, v in chunk] + [None] * (LIN_WIDTH - len(chunk))
-            coefs = [c for c, _ in chunk] + [0] * (LIN_WIDTH - len(chunk))
+            srcs = [v for _, v in chunk] + [None] * (self.lin_width - len(chunk))
+            coefs = [c for c, _ in chunk] + [0] * (self.lin_width - len(chunk))
             out = self._op("lin", srcs, coefs)
         return out
 
@@ -321,7 +322,7 @@ class Prog:
 
         def cost(terms, limit):
             f = lin_form(terms, limit)[0]
-            return FORM_COST[f] if limit == LIN_WIDTH else (0 if f == "unit" else 1000)  # muls operands: unit only
+            return FORM_COST[f] if limit == self.lin_width else (0 if f == "unit" else 1000)  # muls operands: unit only
 
         def fusable(j):
             return j is not None and self.ops[j].kind == "lin" and j not in outs and (uses[j] == 1 or dup)
@@ -337,7 +338,7 @@ class Prog:
                         cand = _norm_terms(terms[:k] + terms[k + 1:] + sub)
                         # a single-use producer disappears (its cost is credited); a shared one
                         # is duplicated into this consumer only if the consumer gets no dearer
-                        credit = cost(self._lin_terms(self.ops[v]), LIN_WIDTH) if uses[v] == 1 else 0
+                        credit = cost(self._lin_terms(self.ops[v]), self.lin_width) if uses[v] == 1 else 0
                         if len(cand) <= limit and all(abs(c3) <= CMAX for c3, _ in cand) and \
                                 cost(cand, limit) <= cost(terms, limit) + credit:
                             uses[v] -= 1
@@ -351,10 +352,10 @@ class Prog:
         for i in sorted(live):
             op = self.ops[i]
             if op.kind == "lin":
-                terms = try_merge(self._lin_terms(op), LIN_WIDTH)
+                terms = try_merge(self._lin_terms(op), self.lin_width)
                 terms = sorted(terms, key=lambda cv: cv[1])
-                op.srcs = tuple([v for _, v in terms] + [None] * (LIN_WIDTH - len(terms)))
-                op.coefs = tuple([c for c, _ in terms] + [0] * (LIN_WIDTH - len(terms)))
+                op.srcs = tuple([v for _, v in terms] + [None] * (self.lin_width - len(terms)))
+                op.coefs = tuple([c for c, _ in terms] + [0] * (self.lin_width - len(terms)))
             elif op.kind == "muls":   # eq keeps single operands: the interpreter tests a - b
                 a, b, c, d = op.srcs
                 ca, cb, cc, cd = op.coefs
@@ -404,10 +405,10 @@ def eval_op(op, vals, inputs, scalar):
 
     def g(i):
         return 0 if s[i] is None else vals[s[i]]
-    if k in ("muls", "lin", "eq"):
+    if k == "lin":
+        return sum(c * g(j) for j, c in enumerate(op.coefs)) % P
+    if k in ("muls", "eq"):
         ca, cb, cc, cd = op.coefs
-        if k == "lin":
-            return (ca * g(0) + cb * g(1) + cc * g(2) + cd * g(3)) % P
         x = (ca * g(0) + cb * g(1)) % P
         y = (cc * g(2) + cd * g(3)) % P
         if k == "muls":

@@ -244,59 +244,73 @@ def _c5(c):
     return c & 31
 
 
+def words_per_lane(prog):
+    """Instruction words per lane per phase: 4 (16 bytes), or 8 for lin_width-8 programs
+    (w4 = E | F << 16, w5 = G | H << 16, w6 = coefficients of E..H, w7 = 0)."""
+    return 8 if prog.lin_width == 8 else 4
+
+
+WIDE_FLAG = 1 << 22   # w0: the lin op uses operands E..H
+
+
 def encode(sc):
-    """-> list of uint32 words, nphases * W * 4."""
+    """-> list of uint32 words, nphases * W * words_per_lane."""
     words = []
     ops = sc.prog.ops
+    nw = words_per_lane(sc.prog)
+    LW = sc.prog.lin_width
     for r in sc.rounds:
         lanes = list(r) + [None] * (sc.W - len(r))
         for i in lanes:
             if i is None:
-                words += [0, 0, 0, 0]
+                words += [0] * nw
                 continue
             op = ops[i]
             k = op.kind
-            s = list(op.srcs) + [None] * (4 - len(op.srcs))
-            coefs = (0, 0, 0, 0)
+            s = list(op.srcs) + [None] * (LW - len(op.srcs))
+            coefs = [0] * LW
+            ext = [None] * 4          # operands E..H (wide programs)
             scale = 0
             if k == "lin":
-                form = lin_form(sc.prog._lin_terms(op), 4)
+                form = lin_form(sc.prog._lin_terms(op), LW)
                 if form[0] == "acc":
-                    A, B, C, D = s
-                    coefs = op.coefs
+                    srcs = list(op.srcs) + [None] * (LW - len(op.srcs))
+                    coefs = list(op.coefs) + [0] * (LW - len(op.coefs))
                 else:
-                    u = form[-1] + [(0, None)] * (4 - len(form[-1]))
-                    A, B, C, D = (v for _, v in u)
-                    coefs = tuple(c for c, _ in u)
+                    u = form[-1] + [(0, None)] * (LW - len(form[-1]))
+                    srcs = [v for _, v in u]
+                    coefs = [c for c, _ in u]
                     if form[0] == "scaled":
                         scale = form[1]
+                A, B, C, D = srcs[:4]
+                if LW == 8:
+                    ext = srcs[4:8]
             elif k == "eq":            # (A - B) * plain 1, flag: zero (fpvm.hpp exec)
-                assert op.coefs == (1, 0, 1, 0) and s[1] is None and s[3] is None, op.coefs
+                assert tuple(op.coefs[:4]) == (1, 0, 1, 0) and s[1] is None and s[3] is None, op.coefs
                 A, B, C, D = s[0], s[2], None, None
-                coefs = (1, -1, 1, 0)
+                coefs[:4] = [1, -1, 1, 0]
             elif k == "muls":
-                A, B, C, D = s
-                coefs = list(op.coefs)
+                A, B, C, D = s[:4]
+                coefs[:4] = list(op.coefs[:4])
                 for h in (0, 2):
                     terms = [(c, v) for c, v in zip(op.coefs[h:h + 2], s[h:h + 2]) if v is not None and c]
                     form = lin_form(terms, 2)
                     assert form[0] == "unit", (k, op.coefs)   # the interpreter's muls operands are unit sums
-                    if form[0] == "unit":
-                        u = form[1] + [(0, None)] * (2 - len(form[1]))
-                        if h == 0:
-                            A, B = u[0][1], u[1][1]
-                        else:
-                            C, D = u[0][1], u[1][1]
-                        coefs[h], coefs[h + 1] = u[0][0], u[1][0]
+                    u = form[1] + [(0, None)] * (2 - len(form[1]))
+                    if h == 0:
+                        A, B = u[0][1], u[1][1]
+                    else:
+                        C, D = u[0][1], u[1][1]
+                    coefs[h], coefs[h + 1] = u[0][0], u[1][0]
             elif k == "sop":           # A C + cb B D
-                A, B, C, D = s
-                coefs = op.coefs
+                A, B, C, D = s[:4]
+                coefs[:4] = list(op.coefs[:4])
             elif k in ("sgn0", "lex"):
                 A, B, C, D = s[0], None, None, None
-                coefs = (1, 0, 1, 0)
+                coefs[:4] = [1, 0, 1, 0]
             elif k in ("inv", "st"):
                 A, B, C, D = s[0], None, None, None
-                coefs = (1, 0, 0, 0)
+                coefs[:4] = [1, 0, 0, 0]
             elif k == "sel":           # A = flag, B = x, C = y
                 A, B, C, D = s[0], s[1], s[2], None
             elif k == "selb":          # B = x, C = y
@@ -307,6 +321,8 @@ def encode(sc):
                 raise ValueError(k)
             dst = sc.slot_of.get(i, 0)
             w0 = OPC[k] | dst << 5 | (op.imm & 63) << 16
+            if LW == 8 and any(coefs[4:8]):
+                w0 |= WIDE_FLAG
             if k in ("sgn0", "lex", "eq"):
                 cref = sc.consts.ref(1, True)          # plain 1: from-Montgomery product
             elif k == "inv":
@@ -315,6 +331,10 @@ def encode(sc):
                 cref = _operand(sc, C)
             w3 = _c5(coefs[0]) | _c5(coefs[1]) << 5 | _c5(coefs[2]) << 10 | _c5(coefs[3]) << 15 | scale << 20
             words += [w0, _operand(sc, A) | _operand(sc, B) << 16, cref | _operand(sc, D) << 16, w3]
+            if nw == 8:
+                e = [_operand(sc, v) for v in ext]
+                w6 = _c5(coefs[4]) | _c5(coefs[5]) << 5 | _c5(coefs[6]) << 10 | _c5(coefs[7]) << 15
+                words += [e[0] | e[1] << 16, e[2] | e[3] << 16, w6, 0]
     return words
 
 
@@ -335,11 +355,13 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
             return const_vals[ref - CONST_BASE][0]
         return slots[ref]
     W = sc.W
+    nw = words_per_lane(sc.prog)
     stored = {}
     for t in range(sc.nrounds):
         results = []
         for lane in range(W):
-            w0, w1, w2, w3 = words[(t * W + lane) * 4:(t * W + lane) * 4 + 4]
+            ins = words[(t * W + lane) * nw:(t * W + lane) * nw + nw]
+            w0, w1, w2, w3 = ins[:4]
             opc = w0 & 31
             if opc == 0:
                 continue
@@ -347,6 +369,12 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
             imm = (w0 >> 16) & 63
             A, B, C, D = get(w1 & 0xFFFF), get(w1 >> 16), get(w2 & 0xFFFF), get(w2 >> 16)
             ca, cb, cc, cd = (_s5((w3 >> (5 * q)) & 31) for q in range(4))
+            ext = 0
+            if nw == 8:
+                w4, w5, w6 = ins[4:7]
+                E, F, G, H = get(w4 & 0xFFFF), get(w4 >> 16), get(w5 & 0xFFFF), get(w5 >> 16)
+                ce, cf, cg, ch = (_s5((w6 >> (5 * q)) & 31) for q in range(4))
+                ext = ce * E + cf * F + cg * G + ch * H
             if opc == OPC["sel"]:
                 z = C if A else B
             elif opc == OPC["selb"]:
@@ -361,7 +389,7 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
             elif opc == OPC["sop"]:
                 z = (A * C + cb * B * D) % P
             elif opc == OPC["lin"]:
-                z = (ca * A + cb * B + cc * C + cd * D) % P
+                z = (ca * A + cb * B + cc * C + cd * D + ext) % P
                 if (w3 >> 20) & 15 > 1:
                     z = z * ((w3 >> 20) & 15) % P
             else:
