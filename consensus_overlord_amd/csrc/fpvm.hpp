@@ -48,12 +48,14 @@ struct Out {
   uint32_t unit;
 };
 constexpr uint32_t CONST_BASE = 0x800;
-// constant-table entries KTAB + n (n = 0..3) hold n (2p + 1) as raw limbs (tools/fpvm/gen.py)
-constexpr uint32_t KTAB = 1;
+// fixed constant-table entries (tools/fpvm/gen.py): 0 the plain 1, 1 the zero, KTAB + n
+// (n = 0..4) n (2p + 1) as raw limbs, the offset of a unit lin with n negated terms
+constexpr uint32_t KZERO = 1, KTAB = 2;
 
 VM_FN void ld_slot(Fp& r, const uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
                    uint32_t ref) {
-  const uint32_t* src = ref >= CONST_BASE ? cst + (ref - CONST_BASE) * 12 : slots + ref * 12;
+  // bit 11 picks the table, the low 11 bits index it (one select + one multiply-add)
+  const uint32_t* src = ((ref & CONST_BASE) ? cst : slots) + (ref & (CONST_BASE - 1)) * 12;
   const uint4* s4 = reinterpret_cast<const uint4*>(src);
   const uint4 a = s4[0], b = s4[1], c = s4[2];
   r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
@@ -120,40 +122,46 @@ VM_FN void scale_reduce(Fp& r, const uint32_t* s, uint32_t k) {
   }
 }
 
-// s (13 limbs, s < 250 p < 2^389) -> r in [0, 2p), r == s mod p.
-VM_FN void reduce2p(Fp& r, const uint32_t* s) {
-  const uint32_t q = quot_est((uint32_t)((((uint64_t)s[12] << 32) | s[11]) >> 7));
-  uint64_t acc = 0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    acc = (uint64_t)q * NP_LIMBS[j] + s[j] + (acc >> 32);
-    r.v[j] = (uint32_t)acc;
-  }
-}
+// 2p + 1 as 12 limbs (2p is even: no carry)
+constexpr uint32_t P2P1_LIMBS[12] = {
+    P2_LIMBS[0] + 1, P2_LIMBS[1], P2_LIMBS[2], P2_LIMBS[3], P2_LIMBS[4], P2_LIMBS[5],
+    P2_LIMBS[6], P2_LIMBS[7], P2_LIMBS[8], P2_LIMBS[9], P2_LIMBS[10], P2_LIMBS[11]};
 
-// acc (13 limbs) += c * X for |c| <= 15, branch-free on the coefficient's value and sign.
-VM_FN void acc_term(uint32_t* acc, const Fp& X, int c) {
-  const uint32_t k = c < 0 ? (uint32_t)(-c) : (uint32_t)c;
-  const uint32_t mask = c < 0 ? 0xFFFFFFFFu : 0u;
-  uint64_t pr = 0;
-  uint32_t cy = c < 0 ? 1u : 0u;  // two's complement: acc + ~prod + 1
+// r = sum_t c_t X_t mod p in [0, 2p) for four X_t < 2p and general |c_t| <= 15 (the final's
+// Granger-Scott combinations 3t +- 2z) in one borrow-free pass of 64-bit products. (Unit sums
+// take lin_sum: v_mad_u64_u32 issues slower than the add chains, measured r02l.)
+// A negative term enters as |c| ~X (xor mask); the offset nw (2p + 1), nw = sum of the negative
+// |c|, turns those into |c| (2p - X) plus nw 2^384, which the final reduction modulo 2^384
+// drops: the true sum s' = sum |c_t| Y_t (Y_t = X_t or 2p - X_t) lies in [0, 120p). Each limb
+// accumulates its column in 64 bits (< 2^38: no carries between terms); q = floor(s'/p) or one
+// less from the top column (the carries into it from below are at most 2^10 units of 2^352,
+// far inside quot_est's margin), then r = s' + q (2^384 - p) modulo 2^384 in one carry pass.
+VM_FN void lin_mad(Fp& r, const Fp& A, const Fp& B, const Fp& C, const Fp& D, int ca, int cb, int cc, int cd) {
+  const Fp* X[4] = {&A, &B, &C, &D};
+  const int cf[4] = {ca, cb, cc, cd};
+  uint64_t acc[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) acc[j] = 0;
+  uint32_t nw = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t a = cf[t] < 0 ? (uint32_t)(-cf[t]) : (uint32_t)cf[t];
+    const uint32_t m = cf[t] < 0 ? ~0u : 0u;
+    nw += a & m;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) acc[j] = (uint64_t)a * (X[t]->v[j] ^ m) + acc[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 12; ++j) acc[j] = (uint64_t)nw * P2P1_LIMBS[j] + acc[j];
+  const int64_t top = (int64_t)(acc[11] >> 7) - ((int64_t)nw << 25);  // s' >> 359, short by <= 8
+  const uint32_t q = top > 0 ? quot_est((uint32_t)top) : 0u;
+  uint64_t cy = 0;
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
-    pr = (uint64_t)X.v[j] * k + (pr >> 32);
-    acc[j] = addc32(acc[j], (uint32_t)pr ^ mask, cy, &cy);
+    const uint64_t v = (uint64_t)q * NP_LIMBS[j] + (acc[j] + cy);
+    r.v[j] = (uint32_t)v;
+    cy = v >> 32;
   }
-  acc[12] = acc[12] + ((uint32_t)(pr >> 32) ^ mask) + cy;
-}
-
-// acc = 256 p (13 limbs): the bias that keeps a signed sum of eight |c| <= 15 terms >= 0
-VM_FN void acc_bias256(uint32_t* acc) {
-  uint32_t prev = 0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    acc[j] = (P_LIMBS[j] << 8) | (prev >> 24);
-    prev = P_LIMBS[j];
-  }
-  acc[12] = prev >> 24;
 }
 
 // Product operands x = A + (nx ? 2p - B : B), y = C + (ny ? 2p - D : D) in [0, 4p), no
@@ -286,41 +294,38 @@ extern bool g_host_any;
 inline bool wave_any(bool p) { return p || g_host_any; }
 #endif
 
-// w0 flag of a wide-program lin op that uses operands E..H (tools/fpvm/sched.py WIDE_FLAG)
-constexpr uint32_t WIDE_FLAG = 1u << 22;
-
-// One phase of one lane. `in` = (w0, A|B<<16, C|D<<16, coefficients of A..D); programs with
-// NW = 8 words per lane also pass `in2` = (E|F<<16, G|H<<16, coefficients of E..H, 0), the
-// operands of up to eight-term linear combinations. The common ops run behind wave-uniform
-// branches (a block runs when any lane of the wave needs it) and each lane stores the result of
-// its own op:
+// One phase of one lane. `in` = (w0, A|B<<16, C|D<<16, coefficients). The common ops run behind
+// wave-uniform branches (a block runs when any lane of the wave needs it) and each lane stores
+// the result of its own op:
 //   products  x = A + cb B, y = C + cd D (unit signs), m = x y: muls; sgn0 / lex / eq take the
 //             from-Montgomery product (y = plain 1; eq: x = A - B) and flag its canonical value;
-//   lin       k (A + cb B + cc C + cd D [+ ce E + ... + ch H]), unit signs, 1 <= k <= 15;
-//   rare      sel, selb, logic, st, inv, lin with general coefficients (per-lane branches).
-template <int NW>
-VM_FN void exec(const uint4 in, const uint4 in2, bool active, uint32_t* __restrict__ slots,
-                const uint32_t* __restrict__ cst, uint64_t scalar, const Out& out) {
-  static_assert(NW == 4 || NW == 8, "instruction words per lane");
+//   linear    lin_mad: k (A + cb B + cc C + cd D) with unit signs, or general coefficients
+//             |c| <= 15, and selb (bit imm of the vote's scalar ? C : B);
+//   rare      sel, logic, st, inv (per-lane branches).
+VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
+                uint64_t scalar, const Out& out) {
   const uint32_t op = active ? (in.x & 31) : (uint32_t)OP_NOP;
   if (!wave_any(op != OP_NOP)) return;
   const uint32_t dst = (in.x >> 5) & 0x7FF;
   const uint32_t imm = (in.x >> 16) & 63;
-  // four operands, always valid references (a missing one is the zero constant)
+  // four operands, always valid references (a missing one is the zero constant); selb (bit imm
+  // of the vote's scalar ? C : B) is a one-term unit lin: A := the picked operand, B = C = 0
+  const bool selb = op == OP_SELB;
+  const bool bit = ((scalar >> imm) & 1) != 0;
+  const uint32_t ra = selb ? (bit ? (in.z & 0xFFFF) : (in.y >> 16)) : (in.y & 0xFFFF);
+  const uint32_t rb = selb ? CONST_BASE + KZERO : in.y >> 16;
+  const uint32_t rc = selb ? CONST_BASE + KZERO : in.z & 0xFFFF;
   Fp A, B, C, D;
-  ld_slot(A, slots, cst, in.y & 0xFFFF);
-  ld_slot(B, slots, cst, in.y >> 16);
-  ld_slot(C, slots, cst, in.z & 0xFFFF);
+  ld_slot(A, slots, cst, ra);
+  ld_slot(B, slots, cst, rb);
+  ld_slot(C, slots, cst, rc);
   ld_slot(D, slots, cst, in.z >> 16);
-  const int ca = ((int)(in.w << 27)) >> 27, cb = ((int)(in.w << 22)) >> 27;
-  const int cc = ((int)(in.w << 17)) >> 27, cd = ((int)(in.w << 12)) >> 27;
-  const bool wide = NW == 8 && (in.x & WIDE_FLAG) != 0;
-  const int ce = NW == 8 ? ((int)(in2.z << 27)) >> 27 : 0, cf = NW == 8 ? ((int)(in2.z << 22)) >> 27 : 0;
-  const int cg = NW == 8 ? ((int)(in2.z << 17)) >> 27 : 0, ch = NW == 8 ? ((int)(in2.z << 12)) >> 27 : 0;
+  const int ca = selb ? 1 : ((int)(in.w << 27)) >> 27, cb = selb ? 0 : ((int)(in.w << 22)) >> 27;
+  const int cc = selb ? 0 : ((int)(in.w << 17)) >> 27, cd = selb ? 0 : ((int)(in.w << 12)) >> 27;
   const bool is_mul = op == OP_MULS || op == OP_SGN0 || op == OP_LEX || op == OP_EQ;
-  const bool lin_unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1 &&
-                        ce >= -1 && ce <= 1 && cf >= -1 && cf <= 1 && cg >= -1 && cg <= 1 && ch >= -1 && ch <= 1;
-  const bool is_lin = op == OP_LIN && lin_unit;
+  const bool lin_unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1;
+  const bool is_lin = (op == OP_LIN && lin_unit) || selb;
+  const bool is_acc = op == OP_LIN && !lin_unit;
   if (wave_any(is_mul)) {
     Fp x, y, m;
     pre_add2(x, A, B, cb < 0, y, C, D, cd < 0, wave_any(is_mul && (cb < 0 || cd < 0)));
@@ -339,25 +344,18 @@ VM_FN void exec(const uint4 in, const uint4 in2, bool active, uint32_t* __restri
   if (wave_any(is_lin)) {
     uint32_t s[13];
     lin_sum(s, A, B, C, D, 1, cb, cc, cd, wave_any(is_lin && (cb < 0 || cc < 0 || cd < 0)), cst);
-    if (NW == 8 && wave_any(is_lin && wide)) {  // second group E..H (all four signed): s < 16p
-      Fp E, F, G, H;
-      ld_slot(E, slots, cst, in2.x & 0xFFFF);
-      ld_slot(F, slots, cst, in2.x >> 16);
-      ld_slot(G, slots, cst, in2.y & 0xFFFF);
-      ld_slot(H, slots, cst, in2.y >> 16);
-      uint32_t s2[13], c = 0;
-      lin_sum(s2, E, F, G, H, ce, cf, cg, ch, wave_any(is_lin && (ce < 0 || cf < 0 || cg < 0 || ch < 0)), cst);
-#pragma unroll
-      for (int j = 0; j < 12; ++j) s[j] = addc32(s[j], s2[j], c, &c);
-      s[12] = c;
-    }
     // "scaled" form k * (unit sum), k < 16 (k <= 1: unchanged)
-    const uint32_t k = (in.w >> 20) & 15;
+    const uint32_t k = selb ? 1u : (in.w >> 20) & 15;
     Fp l;
     scale_reduce(l, s, k > 1 ? k : 1u);
     if (is_lin) st_slot(slots, dst, l);
   }
-  const bool rare = op != OP_NOP && !is_mul && !is_lin;
+  if (wave_any(is_acc)) {  // general coefficients
+    Fp l;
+    lin_mad(l, A, B, C, D, ca, cb, cc, cd);
+    if (is_acc) st_slot(slots, dst, l);
+  }
+  const bool rare = op != OP_NOP && !is_mul && !is_lin && !is_acc;
   if (wave_any(rare)) {
     Fp z = A;
     if (op == OP_ST) {
@@ -365,8 +363,6 @@ VM_FN void exec(const uint4 in, const uint4 in2, bool active, uint32_t* __restri
       uint32_t* b = out.base + (size_t)imm * 12 * out.cap + out.unit;
 #pragma unroll
       for (int k = 0; k < 12; ++k) b[(size_t)k * out.cap] = z.v[k];
-    } else if (op == OP_SELB) {
-      z = ((scalar >> imm) & 1) ? C : B;
     } else if (op == OP_SEL) {
       z = A.v[0] ? C : B;
     } else if (op >= OP_AND && op <= OP_XOR) {
@@ -377,70 +373,36 @@ VM_FN void exec(const uint4 in, const uint4 in2, bool active, uint32_t* __restri
       canon(a, A);
       fp_inv_binary(z, a, C);
 #endif
-    } else if (op == OP_LIN) {  // general coefficients
-      uint32_t acc[13];
-      acc_bias256(acc);
-      acc_term(acc, A, ca);
-      acc_term(acc, B, cb);
-      acc_term(acc, C, cc);
-      acc_term(acc, D, cd);
-      if (NW == 8 && wide) {
-        Fp E;
-        ld_slot(E, slots, cst, in2.x & 0xFFFF);
-        acc_term(acc, E, ce);
-        ld_slot(E, slots, cst, in2.x >> 16);
-        acc_term(acc, E, cf);
-        ld_slot(E, slots, cst, in2.y & 0xFFFF);
-        acc_term(acc, E, cg);
-        ld_slot(E, slots, cst, in2.y >> 16);
-        acc_term(acc, E, ch);
-      }
-      reduce2p(z, acc);
     }
     if (rare && op != OP_ST) st_slot(slots, dst, z);
   }
 }
 
-// Run `nphases` phases of a W-lane program with NW instruction words per lane (the code is
-// phase-major: lane l of phase t at uint4 index (t W + l) NW / 4). Every lane of the workgroup
-// must call this; lanes of inactive slices pass active = false. The VM kernels are single-wave
-// workgroups, so no phase barrier is needed: a wave's LDS operations are performed in issue
-// order, and a slot a phase writes is read from the next phase on (tools/fpvm/sched.py), so the
-// next phase's loads may issue while this phase's stores are still in flight.
+// Run `nphases` phases of a W-lane program (the code is phase-major: lane l of phase t at
+// index t W + l). Every lane of the workgroup must call this; lanes of inactive slices pass
+// active = false. The VM kernels are single-wave workgroups, so no phase barrier is needed: a
+// wave's LDS operations are performed in issue order, and a slot a phase writes is read from the
+// next phase on (tools/fpvm/sched.py), so the next phase's loads may issue while this phase's
+// stores are still in flight.
 #if defined(__HIPCC__)
-template <int NW>
 __device__ __forceinline__ void run(const uint4* __restrict__ code, uint32_t nphases, uint32_t W, uint32_t lane,
                                     bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
                                     uint64_t scalar, const Out& out, uint64_t* __restrict__ trace = nullptr) {
   static_assert(PREFETCH == 4, "prefetch ring below is 4 deep");
-  constexpr uint32_t Q = NW / 4;  // uint4 per lane per phase
   // trace (diagnostics, OVH_FLAG_VM_TRACE): wall clock after every phase
   if (trace && threadIdx.x == 0) trace[0] = wall_clock64();
   // instructions are prefetched PREFETCH phases ahead (an HBM / L2 round trip outlasts a light
   // phase); the code carries PREFETCH trailing NOP phases
-  auto at = [&](uint32_t ph, uint32_t k) { return code[((size_t)ph * W + lane) * Q + k]; };
-  uint4 q0 = at(0, 0), q1 = at(1, 0), q2 = at(2, 0), q3 = at(3, 0);
-  uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0, r2 = r0, r3 = r0;
-  if (Q == 2) {
-    r0 = at(0, 1);
-    r1 = at(1, 1);
-    r2 = at(2, 1);
-    r3 = at(3, 1);
-  }
+  uint4 q0 = code[lane], q1 = code[(size_t)W + lane], q2 = code[(size_t)2 * W + lane],
+        q3 = code[(size_t)3 * W + lane];
 #pragma unroll 1
   for (uint32_t ph = 0; ph < nphases; ++ph) {
-    const uint4 cur = q0, cur2 = r0;
+    const uint4 cur = q0;
     q0 = q1;
     q1 = q2;
     q2 = q3;
-    q3 = at(ph + PREFETCH, 0);
-    if (Q == 2) {
-      r0 = r1;
-      r1 = r2;
-      r2 = r3;
-      r3 = at(ph + PREFETCH, 1);
-    }
-    exec<NW>(cur, cur2, active, slots, cst, scalar, out);
+    q3 = code[(size_t)(ph + PREFETCH) * W + lane];
+    exec(cur, active, slots, cst, scalar, out);
     if (trace) {
       __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (threadIdx.x == 0) trace[ph + 1] = wall_clock64();

@@ -37,7 +37,7 @@
 #include "keygen.hpp"
 #include "sm3.hpp"
 #include "vm_progs.inc"
-static_assert(VM_KTAB == ovh::vm::KTAB, "lin offset table (tools/fpvm/gen.py KTAB)");
+static_assert(VM_KZERO == ovh::vm::KZERO && VM_KTAB == ovh::vm::KTAB, "fixed constants (tools/fpvm/gen.py)");
 
 using namespace ovh;
 
@@ -221,7 +221,7 @@ __device__ __forceinline__ void fold_unit(uint32_t t, uint32_t m, const VmDev& p
     }
   }
   __syncthreads();
-  vm::run<VM_FOLD_NW>(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  vm::run(prog.code, VM_FOLD_NPHASES, VM_FOLD_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
   if (active) {
     for (uint32_t k = lane; k < PART_PLANES; k += VM_FOLD_W) {
       Fp v;
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
     }
   }
   __syncthreads();
-  vm::run<VM_VOTE_NW>(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
+  vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
           vm::Out{s.p, s.cap, i},
           blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) {
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const u
     slot_put(slots, VM_FINAL_IN[k], v.v);
   }
   __syncthreads();
-  vm::run<VM_FINAL_NW>(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0},
+  vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0},
           blockIdx.x == 0 ? prog.trace : nullptr);
   if (lane == 0) *result = slot_flag_get(slots, VM_FINAL_OUT[0]) ? 1 : 0;
 }
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
     }
   }
   __syncthreads();
-  vm::run<VM_VOTE_T_NW>(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
+  vm::run(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
           vm::Out{s.p, s.cap, i}, blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) {
     const uint32_t sf = hdr[0], pf = hdr[1];
@@ -459,7 +459,7 @@ __device__ __forceinline__ bool final_one(uint32_t u, const VmDev& prog, const u
     slot_put(slots, VM_FINAL_IN[k], v.v);
   }
   __syncthreads();
-  vm::run<VM_FINAL_NW>(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
   return slot_flag_get(slots, VM_FINAL_OUT[0]) != 0;
 }
 

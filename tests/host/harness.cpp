@@ -96,9 +96,7 @@ int hx_vm_run(const uint32_t* code, uint32_t nphases, uint32_t W, uint32_t NW, c
   for (uint32_t ph = 0; ph < nphases; ++ph)
     for (uint32_t lane = 0; lane < W; ++lane) {
       const uint32_t* w = code + ((size_t)ph * W + lane) * NW;
-      const uint4 in{w[0], w[1], w[2], w[3]};
-      if (NW == 8) ovh::vm::exec<8>(in, uint4{w[4], w[5], w[6], w[7]}, true, slots, cst, scalar, out);
-      else ovh::vm::exec<4>(in, uint4{0, 0, 0, 0}, true, slots, cst, scalar, out);
+      ovh::vm::exec(uint4{w[0], w[1], w[2], w[3]}, true, slots, cst, scalar, out);
       // the interpreter's lazy-reduction invariant: every slot result lies in [0, 2p)
       const uint32_t op = w[0] & 31, dst = (w[0] >> 5) & 0x7FF;
       if (op != ovh::vm::OP_NOP && op != ovh::vm::OP_ST) {

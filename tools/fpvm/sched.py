@@ -245,12 +245,11 @@ def _c5(c):
 
 
 def words_per_lane(prog):
-    """Instruction words per lane per phase: 4 (16 bytes), or 8 for lin_width-8 programs
-    (w4 = E | F << 16, w5 = G | H << 16, w6 = coefficients of E..H, w7 = 0)."""
-    return 8 if prog.lin_width == 8 else 4
-
-
-WIDE_FLAG = 1 << 22   # w0: the lin op uses operands E..H
+    """Instruction words per lane per phase (16 bytes). The 32-byte format with eight-operand
+    lin ops (lin_width 8) was measured slower and the interpreter no longer decodes it."""
+    if prog.lin_width != 4:
+        raise ValueError("%s: the interpreter runs 4-operand lin ops only" % prog.name)
+    return 4
 
 
 def encode(sc):
@@ -321,8 +320,6 @@ def encode(sc):
                 raise ValueError(k)
             dst = sc.slot_of.get(i, 0)
             w0 = OPC[k] | dst << 5 | (op.imm & 63) << 16
-            if LW == 8 and any(coefs[4:8]):
-                w0 |= WIDE_FLAG
             if k in ("sgn0", "lex", "eq"):
                 cref = sc.consts.ref(1, True)          # plain 1: from-Montgomery product
             elif k == "inv":
@@ -331,10 +328,6 @@ def encode(sc):
                 cref = _operand(sc, C)
             w3 = _c5(coefs[0]) | _c5(coefs[1]) << 5 | _c5(coefs[2]) << 10 | _c5(coefs[3]) << 15 | scale << 20
             words += [w0, _operand(sc, A) | _operand(sc, B) << 16, cref | _operand(sc, D) << 16, w3]
-            if nw == 8:
-                e = [_operand(sc, v) for v in ext]
-                w6 = _c5(coefs[4]) | _c5(coefs[5]) << 5 | _c5(coefs[6]) << 10 | _c5(coefs[7]) << 15
-                words += [e[0] | e[1] << 16, e[2] | e[3] << 16, w6, 0]
     return words
 
 

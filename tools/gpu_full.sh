@@ -17,4 +17,7 @@ if [ -n "${PMC:-}" ]; then
   timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY \
     SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/pmc_sq" -o sq --output-format csv -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-latency > "$OUT/pmc_sq.log" 2>&1
 fi
+if [ -n "${TRACE:-}" ]; then
+  cd "$R" && timeout -k 10 200 python -u tools/vm_trace.py "$OUT/trace" > "$OUT/trace.log" 2>&1
+fi
 echo done > "$OUT/ok"
