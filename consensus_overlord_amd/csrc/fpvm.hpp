@@ -285,13 +285,17 @@ VM_FN void fp_inv_binary(Fp& r, const Fp& a, const Fp& r3) {
   fp_mul(r, limbs_is_one(u) ? x1 : x2, r3);
 }
 
+// phase header bits (w0 bits 22..28, tools/fpvm/sched.py H_*)
+constexpr uint32_t H_MUL = 1u << 22, H_MULNEG = 1u << 23, H_FLAG = 1u << 24, H_LIN = 1u << 25,
+                   H_LINNEG = 1u << 26, H_ACC = 1u << 27, H_RARE = 1u << 28;
+constexpr uint32_t H_ANY = H_MUL | H_LIN | H_ACC | H_RARE;
 #if defined(__HIPCC__)
-VM_FN bool wave_any(bool p) { return __ballot(p) != 0; }
+// the header is the same in every lane: read it once into an SGPR
+VM_FN uint32_t uniform(uint32_t w0) { return __builtin_amdgcn_readfirstlane(w0); }
 #else
-// host emulation runs one lane at a time; with g_host_any set every wave-uniform block runs
-// for every lane (the device behaviour when any other lane of the wave needs the block)
-extern bool g_host_any;
-inline bool wave_any(bool p) { return p || g_host_any; }
+// host emulation runs one lane at a time with the phase's header: a block runs for every lane
+// when any lane of the phase needs it, as on the device
+inline uint32_t uniform(uint32_t w0) { return w0; }
 #endif
 
 // One phase of one lane. `in` = (w0, A|B<<16, C|D<<16, coefficients). The common ops run behind
@@ -305,7 +309,10 @@ inline bool wave_any(bool p) { return p || g_host_any; }
 VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
                 uint64_t scalar, const Out& out) {
   const uint32_t op = active ? (in.x & 31) : (uint32_t)OP_NOP;
-  if (!wave_any(op != OP_NOP)) return;
+  // the phase header (bits 22.. of w0, equal in every lane; tools/fpvm/sched.py phase_bits) names
+  // the blocks some lane of the phase needs: scalar branches, no ballots
+  const uint32_t hdr = uniform(in.x);
+  if (!(hdr & H_ANY)) return;
   const uint32_t dst = (in.x >> 5) & 0x7FF;
   const uint32_t imm = (in.x >> 16) & 63;
   // four operands, always valid references (a missing one is the zero constant); selb (bit imm
@@ -326,12 +333,12 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
   const bool lin_unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1;
   const bool is_lin = (op == OP_LIN && lin_unit) || selb;
   const bool is_acc = op == OP_LIN && !lin_unit;
-  if (wave_any(is_mul)) {
+  if (hdr & H_MUL) {
     Fp x, y, m;
-    pre_add2(x, A, B, cb < 0, y, C, D, cd < 0, wave_any(is_mul && (cb < 0 || cd < 0)));
+    pre_add2(x, A, B, cb < 0, y, C, D, cd < 0, (hdr & H_MULNEG) != 0);
     fp_mul(m, x, y);
     const bool flag = is_mul && op != OP_MULS;
-    if (wave_any(flag)) {  // m is canonical here: y = 1, x < 4p -> x / 2^384 + p rounds to <= p
+    if (hdr & H_FLAG) {  // m is canonical here: y = 1, x < 4p -> x / 2^384 + p rounds to <= p
       uint32_t f = 0;
       if (op == OP_SGN0) f = m.v[0] & 1u;
       if (op == OP_LEX) f = limbs_gt(m.v, HALF_P) ? 1u : 0u;
@@ -341,22 +348,22 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
     }
     if (is_mul) st_slot(slots, dst, m);
   }
-  if (wave_any(is_lin)) {
+  if (hdr & H_LIN) {
     uint32_t s[13];
-    lin_sum(s, A, B, C, D, 1, cb, cc, cd, wave_any(is_lin && (cb < 0 || cc < 0 || cd < 0)), cst);
+    lin_sum(s, A, B, C, D, 1, cb, cc, cd, (hdr & H_LINNEG) != 0, cst);
     // "scaled" form k * (unit sum), k < 16 (k <= 1: unchanged)
     const uint32_t k = selb ? 1u : (in.w >> 20) & 15;
     Fp l;
     scale_reduce(l, s, k > 1 ? k : 1u);
     if (is_lin) st_slot(slots, dst, l);
   }
-  if (wave_any(is_acc)) {  // general coefficients
+  if (hdr & H_ACC) {  // general coefficients
     Fp l;
     lin_mad(l, A, B, C, D, ca, cb, cc, cd);
     if (is_acc) st_slot(slots, dst, l);
   }
   const bool rare = op != OP_NOP && !is_mul && !is_lin && !is_acc;
-  if (wave_any(rare)) {
+  if (hdr & H_RARE) {
     Fp z = A;
     if (op == OP_ST) {
       canon(z, A);

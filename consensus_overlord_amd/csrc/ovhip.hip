@@ -233,6 +233,22 @@ __device__ __forceinline__ void fold_unit(uint32_t t, uint32_t m, const VmDev& p
   }
 }
 
+// The vote waves of a CU run the same program in near lockstep, so every phase's operand loads
+// (12 KB per wave) reach the CU's LDS at the same moment. OVH_VOTE_STAGGER > 0 offsets the start
+// of the wave on SIMD s by s x OVH_VOTE_STAGGER x 64 cycles (the offset persists: every wave's
+// phases take equally long), spreading those bursts.
+#ifndef OVH_VOTE_STAGGER
+#define OVH_VOTE_STAGGER 0
+#endif
+__device__ __forceinline__ void vote_stagger() {
+#if OVH_VOTE_STAGGER > 0
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID, all 32 bits
+  const uint32_t n = ((hw >> 4) & 3) * OVH_VOTE_STAGGER;          // SIMD_ID
+#pragma unroll 1
+  for (uint32_t k = 0; k < n; ++k) __builtin_amdgcn_s_sleep(1);
+#endif
+}
+
 // Per vote: VM "vote" program + reference-precedence code + the vote's (f, r sigma)
 // contribution. LDS: constants, then VM_SLICES x (VM_VOTE_NSLOTS slots).
 __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
@@ -274,6 +290,7 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
     }
   }
   __syncthreads();
+  vote_stagger();
   vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
           vm::Out{s.p, s.cap, i},
           blockIdx.x == 0 ? prog.trace : nullptr);
@@ -408,6 +425,7 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
     }
   }
   __syncthreads();
+  vote_stagger();
   vm::run(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
           vm::Out{s.p, s.cap, i}, blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) {

@@ -7,8 +7,6 @@
 
 using namespace ovh;
 
-bool ovh::vm::g_host_any = false;
-
 static const uint8_t DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_";
 
 extern "C" {
@@ -87,16 +85,17 @@ int hx_g1_subgroup(const uint8_t* in, uint32_t len) {
 // One slice of an Fp-VM program through the interpreter (fpvm.hpp exec), lane by lane in each
 // phase (a phase's writes never target a slot that phase reads: tools/fpvm/sched.py).
 // slots: nslots x 12 words (in/out); planes: `st` output planes, 12 words each.
-// any_all = 1 runs every wave-uniform block for every lane.
+// any_all = 1 runs every wave-uniform block for every lane (all phase-header bits set).
 int hx_vm_run(const uint32_t* code, uint32_t nphases, uint32_t W, uint32_t NW, const uint32_t* cst, uint32_t* slots,
               uint64_t scalar, uint32_t* planes, uint32_t nplanes, int any_all) {
-  ovh::vm::g_host_any = any_all != 0;
+  using namespace ovh::vm;
+  const uint32_t all = any_all ? (H_MUL | H_MULNEG | H_FLAG | H_LIN | H_LINNEG | H_ACC | H_RARE) : 0u;
   const ovh::vm::Out out{planes, 1, 0};
   (void)nplanes;
   for (uint32_t ph = 0; ph < nphases; ++ph)
     for (uint32_t lane = 0; lane < W; ++lane) {
       const uint32_t* w = code + ((size_t)ph * W + lane) * NW;
-      ovh::vm::exec(uint4{w[0], w[1], w[2], w[3]}, true, slots, cst, scalar, out);
+      ovh::vm::exec(uint4{w[0] | all, w[1], w[2], w[3]}, true, slots, cst, scalar, out);
       // the interpreter's lazy-reduction invariant: every slot result lies in [0, 2p)
       const uint32_t op = w[0] & 31, dst = (w[0] >> 5) & 0x7FF;
       if (op != ovh::vm::OP_NOP && op != ovh::vm::OP_ST) {

@@ -8,7 +8,8 @@ one slot; results are visible from phase t + 1. A slot whose value was last read
 be rewritten from phase t + 1 on.
 
 Instruction (4 x uint32 per lane per phase):
-  w0 = opcode | dst << 5 (11 bits) | imm << 16 (6 bits)
+  w0 = opcode | dst << 5 (11 bits) | imm << 16 (6 bits) | phase header << 22 (the same in every
+       lane: which interpreter blocks the phase needs, phase_bits)
   w1 = A | B << 16,  w2 = C | D << 16
   w3 = ca | cb << 5 | cc << 10 | cd << 15   (5-bit two's-complement coefficients)
        (sop: z = A C + cb B D)
@@ -77,7 +78,7 @@ class Scheduled:
 
 
 def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1, mixed=True, slot_target=None,
-             hoist=None, stretch=1.3):
+             hoist=None, stretch=1.3, split_sop=False, dual=False, bias=None):
     ops = prog.ops
     live = prog.live_ops()
     liveset = set(live)
@@ -97,6 +98,10 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
         prio[i] = c + max((prio[s] for s in succs[i]), default=0)
         if ops[i].kind == "st":
             prio[i] = 10 ** 6   # stores free their slot: run them as soon as they are ready
+    if bias is not None:   # per-op priority offsets (staggering the units of a merged program)
+        for i in work:
+            if ops[i].kind != "st":
+                prio[i] += bias.get(i, 0)
     # release phase: an op may not run more than `hoist` phases before the earliest phase its
     # first consumer could run (ASAP depth x the schedule's expected stretch), so values that
     # are ready early but needed late (the per-step addends of a scalar-multiplication chain)
@@ -155,12 +160,23 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
         wait_l = [i for i in ready_l if i not in set(el)]
         top_h = max((prio[i] for i in eh), default=-1)
         top_l = max((prio[i] for i in el), default=-1)
-        if top_l > top_h or not eh:
+        if dual:   # every lane runs one heavy and one light op per phase
+            kind = "H" if eh else "L"
+            cur = pick(eh, W, pressure) + pick(el, W, pressure)
+        elif top_l > top_h or not eh:
             kind = "L"
             cur = pick(el, W, pressure)
         else:
             kind = "H"
-            cur = pick(eh, W, pressure)
+            if split_sop:   # a phase runs sops or products, never both (the wave would pay for both)
+                fam = max(eh, key=lambda i: prio[i])
+                fam = ops[fam].kind == "sop"
+                same = [i for i in eh if (ops[i].kind == "sop") == fam]
+                other = [i for i in eh if (ops[i].kind == "sop") != fam]
+                cur = pick(same, W, pressure)
+                eh = same + other
+            else:
+                cur = pick(eh, W, pressure)
             if mixed:
                 cur += pick(el, W - len(cur), pressure)
         ready_h[:] = eh + wait_h
@@ -328,7 +344,35 @@ def encode(sc):
                 cref = _operand(sc, C)
             w3 = _c5(coefs[0]) | _c5(coefs[1]) << 5 | _c5(coefs[2]) << 10 | _c5(coefs[3]) << 15 | scale << 20
             words += [w0, _operand(sc, A) | _operand(sc, B) << 16, cref | _operand(sc, D) << 16, w3]
+        # the phase header (wave-uniform code paths) in bits 22.. of every lane's w0
+        base = len(words) - sc.W * nw
+        hdr = 0
+        for lane in range(sc.W):
+            hdr |= phase_bits(words[base + lane * nw:base + lane * nw + 4])
+        for lane in range(sc.W):
+            words[base + lane * nw] |= hdr
     return words
+
+
+# phase header bits (fpvm.hpp exec): which interpreter blocks any lane of the phase needs
+H_MUL, H_MULNEG, H_FLAG, H_LIN, H_LINNEG, H_ACC, H_RARE = (1 << k for k in range(22, 29))
+
+
+def phase_bits(w):
+    """Header bits one lane's instruction (w0..w3) contributes (mirrors fpvm.hpp exec)."""
+    opc = w[0] & 31
+    if opc == OPC["nop"]:
+        return 0
+    ca, cb, cc, cd = (_s5((w[3] >> (5 * q)) & 31) for q in range(4))
+    if opc in (OPC["muls"], OPC["sgn0"], OPC["lex"], OPC["eq"]):
+        return H_MUL | (H_MULNEG if cb < 0 or cd < 0 else 0) | (0 if opc == OPC["muls"] else H_FLAG)
+    if opc == OPC["selb"]:
+        return H_LIN
+    if opc == OPC["lin"]:
+        if ca == 1 and all(-1 <= c <= 1 for c in (cb, cc, cd)):
+            return H_LIN | (H_LINNEG if min(cb, cc, cd) < 0 else 0)
+        return H_ACC
+    return H_RARE
 
 
 def _s5(x):

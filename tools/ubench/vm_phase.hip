@@ -4,11 +4,13 @@
 //   hipcc -O3 --offload-arch=gfx950 -o /tmp/vm_phase tools/ubench/vm_phase.hip && /tmp/vm_phase
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <vector>
 
 #include "../../consensus_overlord_amd/csrc/fpvm.hpp"
+#include "../../consensus_overlord_amd/csrc/vm_progs.inc"
 
-namespace ovh { namespace vm { constexpr uint32_t ABSENT = CONST_BASE; } }
+namespace ovh { namespace vm { constexpr uint32_t ABSENT = CONST_BASE + KZERO; } }
 
 using namespace ovh;
 
@@ -25,14 +27,14 @@ constexpr int NSLOT = 64;
 
 __global__ __launch_bounds__(64) void k_vm(const uint4* code, uint32_t nph, uint32_t W, const uint32_t* cst_g,
                                            uint32_t* out) {
-  __shared__ uint32_t lds[4 * 12 + 4 * NSLOT * 12];
+  __shared__ uint32_t lds[VM_NCONST * 12 + 4 * NSLOT * 12];
   uint32_t* cst = lds;
-  if (threadIdx.x < 48) cst[threadIdx.x] = cst_g[threadIdx.x];
+  for (uint32_t k = threadIdx.x; k < VM_NCONST * 12; k += 64) cst[k] = cst_g[k];
   const uint32_t slice = threadIdx.x / W, lane = threadIdx.x % W;
-  uint32_t* slots = lds + 48 + slice * NSLOT * 12;
+  uint32_t* slots = lds + VM_NCONST * 12 + slice * NSLOT * 12;
   for (int k = 0; k < 12; ++k) slots[lane * 12 + k] = (k == 0) ? (lane + 3) : (k < 11 ? 0x1234567u * (lane + k) : 0);
   __syncthreads();
-  vm::run(code, nph, W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  vm::run(code, nph, W, lane, true, slots, cst, 0x5555aaaa5555aaaaull, vm::Out{nullptr, 0, 0});
   if (lane == 0) out[blockIdx.x * 64 + threadIdx.x] = slots[0];
 }
 
@@ -48,20 +50,25 @@ __global__ __launch_bounds__(64) void k_chain(uint32_t iters, uint32_t* out) {
 
 static uint32_t w0(uint32_t op, uint32_t dst) { return op | dst << 5; }
 
-int main() {
+int main(int argc, char** argv) {
+  // optional: vm_phase KIND W GRID -> that one case only (for PMC passes)
+  const int only_kind = argc > 3 ? atoi(argv[1]) : -1;
+  const uint32_t only_w = argc > 3 ? (uint32_t)atoi(argv[2]) : 0, only_grid = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
   const uint32_t NPH = 2048;
-  std::vector<uint32_t> cst(48, 0);
   uint32_t *d_cst, *d_out;
-  CHECK(hipMalloc(&d_cst, 48 * 4));
-  CHECK(hipMemcpy(d_cst, cst.data(), 48 * 4, hipMemcpyHostToDevice));
+  CHECK(hipMalloc(&d_cst, sizeof(VM_CONST_WORDS)));
+  CHECK(hipMemcpy(d_cst, VM_CONST_WORDS, sizeof(VM_CONST_WORDS), hipMemcpyHostToDevice));
   CHECK(hipMalloc(&d_out, 64 * 8192 * 4));
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  const char* names[] = {"nop", "lin", "muls", "muls_half_lanes", "lin_coef", "muls_preadd"};
+  const char* names[] = {"nop", "lin", "muls", "muls_half_lanes", "lin_coef", "muls_preadd", "lin4_neg", "selb",
+                         "muls+lin4"};
   for (uint32_t W : {16u, 64u}) {
-    for (int kind = 0; kind < 6; ++kind) {
-      std::vector<uint32_t> code((size_t)(NPH + 2) * W * 4, 0);
+    if (only_kind >= 0 && W != only_w) continue;
+    for (int kind = 0; kind < 9; ++kind) {
+      if (only_kind >= 0 && kind != only_kind) continue;
+      std::vector<uint32_t> code((size_t)(NPH + vm::PREFETCH) * W * 4, 0);
       for (uint32_t ph = 0; ph < NPH; ++ph)
         for (uint32_t l = 0; l < W; ++l) {
           uint32_t* c = &code[((size_t)ph * W + l) * 4];
@@ -81,7 +88,17 @@ int main() {
             c[1] = l | src << 16;
             c[2] = ((l + 2) % W) | ((l + 3) % W) << 16;
             c[3] = 1 | 1 << 5 | 1 << 10 | (32 - 1) << 15;  // (a + b)(c - d)
-          } else if (kind >= 2 && kind <= 3 && (kind == 2 || l % 2 == 0)) {
+          } else if (kind == 6 || (kind == 8 && l % 2 == 1)) {
+            c[0] = w0(vm::OP_LIN, l);
+            c[1] = l | src << 16;
+            c[2] = ((l + 2) % W) | ((l + 3) % W) << 16;
+            c[3] = 1 | (32 - 1) << 5 | 1 << 10 | (32 - 1) << 15;  // a - b + c - d
+          } else if (kind == 7) {
+            c[0] = w0(vm::OP_SELB, l) | (l % 64) << 16;
+            c[1] = vm::ABSENT | src << 16;
+            c[2] = ((l + 2) % W) | vm::ABSENT << 16;
+            c[3] = 0;
+          } else if ((kind >= 2 && kind <= 3 && (kind == 2 || l % 2 == 0)) || kind == 8) {
             c[0] = w0(vm::OP_MULS, l);
             c[1] = l | vm::ABSENT << 16;
             c[2] = src | vm::ABSENT << 16;
@@ -91,7 +108,8 @@ int main() {
       uint4* d_code;
       CHECK(hipMalloc(&d_code, code.size() * 4));
       CHECK(hipMemcpy(d_code, code.data(), code.size() * 4, hipMemcpyHostToDevice));
-      for (uint32_t grid : {256u, 1024u, 2048u, 4096u}) {
+      for (uint32_t grid : {256u, 1024u, 2048u}) {
+        if (only_kind >= 0 && grid != only_grid) continue;
         hipLaunchKernelGGL(k_vm, dim3(grid), dim3(64), 0, 0, d_code, NPH, W, d_cst, d_out);
         CHECK(hipDeviceSynchronize());
         CHECK(hipEventRecord(a));
@@ -106,6 +124,7 @@ int main() {
       CHECK(hipFree(d_code));
     }
   }
+  if (only_kind >= 0) return 0;
   for (uint32_t grid : {256u, 1024u, 2048u, 4096u, 8192u}) {
     const uint32_t iters = 4096;
     hipLaunchKernelGGL(k_chain, dim3(grid), dim3(64), 0, 0, iters, d_out);
