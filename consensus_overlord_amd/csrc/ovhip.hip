@@ -769,10 +769,12 @@ struct ovh_ctx {
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
   // pipelined batches (ovh_verify_batch_device_async): the final check + bisection of batch k
-  // run on fstream while batch k + 1's per-vote stages run on stream; OVH_BATCH_SLOTS slots of
-  // batch state rotate (a slot is reused only after its final-stream work finished).
-  hipStream_t fstream = nullptr;
-  hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of each slot (all == fstream, see ovh_create)
+  // run on a final stream while batch k + 1's per-vote stages run on stream; OVH_BATCH_SLOTS
+  // slots of batch state rotate (a slot is reused only after its final-stream work finished).
+  // Batches alternate between two final streams, so two finals may run at once (each shares a
+  // SIMD with a vote wave and takes longer than a vote kernel there).
+  hipStream_t fstream = nullptr, fstream2 = nullptr;
+  hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
   hipStream_t hstream = nullptr;  // hash_to_field of the next batch, beside the current vote
   hipEvent_t ev_h[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
@@ -839,6 +841,11 @@ static_assert(VM_VOTE_W * VM_SLICES == 64 && VM_VOTE_T_W * VM_SLICES == 64 && VM
                   VM_FINAL_W == 64, "VM slice widths");
 static constexpr size_t LDS_FOLD1 = (size_t)VM_NCONST * 48 + (size_t)VM_FOLD_NSLOTS * 48;
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
+// a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
+// allocation granules assumed)
+constexpr size_t lds_granule(size_t b) { return (b + 1023) / 1024 * 1024; }
+static_assert(4 * lds_granule(LDS_VOTE > LDS_VOTE_T ? LDS_VOTE : LDS_VOTE_T) + 2 * lds_granule(LDS_FINAL) <= 160 * 1024,
+              "four vote workgroups + two finals per CU");
 static_assert(VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_NSLOTS * 12 + 4) &&
                   VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_T_NSLOTS * 12 + 4),
               "fused fold reuses the vote slots");
@@ -926,6 +933,7 @@ static Slab region_S(ovh_ctx* c, int slot, int r) {
 static int sync_all(ovh_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->fstream));
+  HIPCHK(hipStreamSynchronize(c->fstream2));
   HIPCHK(hipStreamSynchronize(c->hstream));
   return 0;
 }
@@ -992,8 +1000,10 @@ static int ensure_in(ovh_ctx* c, size_t bytes) {
 // Batch state slot k for the next batch on the main stream: the stream first waits until the
 // final stream has finished with the slot's previous batch (its bisection reads that state).
 static int take_slot(ovh_ctx* c, int* slot) {
-  const int k = (int)(c->pipe_k++ % OVH_BATCH_SLOTS);
+  const int k = (int)(c->pipe_k % OVH_BATCH_SLOTS);
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_back[k], 0));
+  c->fs[k] = (c->pipe_k & 1) ? c->fstream2 : c->fstream;
+  ++c->pipe_k;
   c->last_slot = k;
   *slot = k;
   return 0;
@@ -1121,11 +1131,12 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
   CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, true));
   uint32_t m = groups_of((uint32_t)n);
   int reg = 1;
-  CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 64));
+  // every fold level on the main stream (it idles while a final runs): the final streams carry
+  // only the finals and the bisections, and no fold workgroup competes with a vote for LDS
+  CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 4));
   HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
   hipStream_t fst = c->fs[slot];
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
-  CHK(fold_down(c, slot, fst, 1, &reg, &m, 4));
   int32_t* verdict = c->result + RES_BATCH + slot;
   enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict);
   enqueue_bisect(c, fst, slot, (uint32_t)n, d_codes, verdict);
@@ -1349,15 +1360,15 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   bool ok = xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
-            (c->fs[0] = c->fstream) != nullptr &&
+            hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
             hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->part_out, 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
             hipMemset(c->result, 0, 64) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
-  // one final stream for all slots: a final shares a SIMD with a vote wave and runs at half
-  // speed there; with two in flight (3 slots, a stream each: r02i) every third vote kernel lost
-  // 2.4 ms to a workgroup that found no LDS beside two finals and a fold
-  for (int k = 1; ok && k < OVH_BATCH_SLOTS; ++k) c->fs[k] = c->fstream;
+  // two finals in flight at most (LDS budget below: four vote workgroups and two finals fit a
+  // CU; r02i ran one final stream per slot and lost 2.4 ms in every third vote kernel to a
+  // workgroup that found no LDS beside two finals and a final-stream fold)
+  for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k) c->fs[k] = c->fstream;
   for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k)
     ok = hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_h[k], hipEventDisableTiming) == hipSuccess &&
@@ -1407,7 +1418,8 @@ static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   for (hipStream_t s : {c->stream, c->hstream})
     if (s) (void)hipStreamSynchronize(s);
-  if (c->fstream) (void)hipStreamSynchronize(c->fstream);
+  for (hipStream_t s : {c->fstream, c->fstream2})
+    if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k]})
       if (p) (void)hipFree(p);
@@ -1427,7 +1439,8 @@ static void destroy_one(ovh_ctx* c) {
   }
   for (hipStream_t s : {c->stream, c->hstream})
     if (s) (void)hipStreamDestroy(s);
-  if (c->fstream) (void)hipStreamDestroy(c->fstream);
+  for (hipStream_t s : {c->fstream, c->fstream2})
+    if (s) (void)hipStreamDestroy(s);
   delete c;
 }
 

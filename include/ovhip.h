@@ -173,7 +173,7 @@ int ovh_batch_fallback_device(ovh_ctx* ctx, size_t n, int32_t* d_codes);
  * k + 1's per-vote work. Up to OVH_BATCH_SLOTS batches may be in flight per context; the
  * d_codes of a batch must stay untouched until ovh_batch_wait returns, after which they hold
  * exactly the per-vote ovh_verify results. */
-#define OVH_BATCH_SLOTS 2 /* batches in flight per context (state slots) */
+#define OVH_BATCH_SLOTS 3 /* batches in flight per context (state slots) */
 int ovh_verify_batch_device_async(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
                                   const uint8_t* d_pks, int32_t* d_codes);
 int ovh_batch_wait(ovh_ctx* ctx);

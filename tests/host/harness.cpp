@@ -82,6 +82,15 @@ int hx_g1_subgroup(const uint8_t* in, uint32_t len) {
   return g1_in_subgroup(j) ? 1 : 0;
 }
 
+// The VM's modular inverse (fpvm.hpp fp_inv) on a raw canonical value: r3 = raw R turns the
+// closing Montgomery product into the identity, so out = a^-1 mod p (0 -> 0).
+void hx_fp_inv_raw(const uint32_t* a, const uint32_t* r_raw, uint32_t* out) {
+  Fp x, r, rr;
+  for (int k = 0; k < 12; ++k) x.v[k] = a[k], rr.v[k] = r_raw[k];
+  ovh::vm::fp_inv(r, x, rr);
+  for (int k = 0; k < 12; ++k) out[k] = r.v[k];
+}
+
 // One slice of an Fp-VM program through the interpreter (fpvm.hpp exec), lane by lane in each
 // phase (a phase's writes never target a slot that phase reads: tools/fpvm/sched.py).
 // slots: nslots x 12 words (in/out); planes: `st` output planes, 12 words each.

@@ -152,3 +152,23 @@ def test_fold_final_bisect_on_interpreter(hx, built, golden_votes, any_all):  # 
         sim = sched.simulate(psc, pwords, pin)
         assert sim == {"ok": want}
         assert_same(run_vm(hx, consts, psc, pwords, pin, 0, any_all), sim, "final/bisect")
+
+
+def test_fp_inv(hx):
+    """fpvm.hpp fp_inv (Bernstein-Yang divsteps, the final program's inv op) against pow(a, -1, p)
+    on edge values and seeded random ones, including values with long runs of zero / one bits."""
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    hx.hx_fp_inv_raw.argtypes = [u32p, u32p, u32p]
+    rr = np.array(_words(R), dtype=np.uint32)
+    rng = np.random.default_rng(0xB1A5)
+    vals = [0, 1, 2, 3, P - 1, P - 2, (P - 1) // 2, (P + 1) // 2, 2 ** 380, 2 ** 381 - 1 - P + P // 3,
+            (1 << 32) - 1, 1 << 200, P - (1 << 300)]
+    vals += [int.from_bytes(rng.bytes(48), "little") % P for _ in range(400)]
+    vals += [int.from_bytes(rng.bytes(48), "little") % (1 << int(rng.integers(1, 381))) for _ in range(100)]
+    for a in vals:
+        a %= P
+        out = np.zeros(12, dtype=np.uint32)
+        hx.hx_fp_inv_raw(np.array(_words(a), dtype=np.uint32).ctypes.data_as(u32p), rr.ctypes.data_as(u32p),
+                         out.ctypes.data_as(u32p))
+        got = sum(int(w) << (32 * k) for k, w in enumerate(out))
+        assert got == (pow(a, -1, P) if a else 0), hex(a)

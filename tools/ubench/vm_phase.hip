@@ -38,6 +38,28 @@ __global__ __launch_bounds__(64) void k_vm(const uint4* code, uint32_t nph, uint
   if (lane == 0) out[blockIdx.x * 64 + threadIdx.x] = slots[0];
 }
 
+// run() with every phase fetching the SAME code block (period 1): the instruction stream always
+// hits in cache; compared with k_vm it prices the code-fetch latency the 1-phase prefetch exposes
+__global__ __launch_bounds__(64) void k_vm_samecode(const uint4* code, uint32_t nph, uint32_t W, const uint32_t* cst_g,
+                                                    uint32_t* out) {
+  __shared__ uint32_t lds[VM_NCONST * 12 + 4 * NSLOT * 12];
+  uint32_t* cst = lds;
+  for (uint32_t k = threadIdx.x; k < VM_NCONST * 12; k += 64) cst[k] = cst_g[k];
+  const uint32_t slice = threadIdx.x / W, lane = threadIdx.x % W;
+  uint32_t* slots = lds + VM_NCONST * 12 + slice * NSLOT * 12;
+  for (int k = 0; k < 12; ++k) slots[lane * 12 + k] = (k == 0) ? (lane + 3) : (k < 11 ? 0x1234567u * (lane + k) : 0);
+  __syncthreads();
+  uint4 q = code[lane];
+#pragma unroll 1
+  for (uint32_t ph = 0; ph < nph; ++ph) {
+    const uint4 cur = q;
+    q = code[lane + (ph & 1) * 0];
+    vm::exec(cur, true, slots, cst, 0x5555aaaa5555aaaaull, vm::Out{nullptr, 0, 0});
+  }
+  __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) out[blockIdx.x * 64 + threadIdx.x] = slots[0];
+}
+
 __global__ __launch_bounds__(64) void k_chain(uint32_t iters, uint32_t* out) {
   Fp x, y;
   for (int k = 0; k < 12; ++k) {
@@ -49,6 +71,24 @@ __global__ __launch_bounds__(64) void k_chain(uint32_t iters, uint32_t* out) {
 }
 
 static uint32_t w0(uint32_t op, uint32_t dst) { return op | dst << 5; }
+
+static int s5(uint32_t x) { return (x & 16) ? (int)x - 32 : (int)x; }
+
+// phase header bits of one lane (tools/fpvm/sched.py phase_bits)
+static uint32_t phase_bits(const uint32_t* w) {
+  using namespace vm;
+  const uint32_t opc = w[0] & 31;
+  if (opc == OP_NOP) return 0;
+  const int ca = s5(w[3] & 31), cb = s5((w[3] >> 5) & 31), cc = s5((w[3] >> 10) & 31), cd = s5((w[3] >> 15) & 31);
+  if (opc == OP_MULS || opc == OP_SGN0 || opc == OP_LEX || opc == OP_EQ)
+    return H_MUL | ((cb < 0 || cd < 0) ? H_MULNEG : 0) | (opc == OP_MULS ? 0 : H_FLAG);
+  if (opc == OP_SELB) return H_LIN;
+  if (opc == OP_LIN) {
+    const bool unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1;
+    return unit ? (H_LIN | ((cb < 0 || cc < 0 || cd < 0) ? H_LINNEG : 0)) : H_ACC;
+  }
+  return H_RARE;
+}
 
 int main(int argc, char** argv) {
   // optional: vm_phase KIND W GRID -> that one case only (for PMC passes)
@@ -105,6 +145,11 @@ int main(int argc, char** argv) {
             c[3] = 1 | 1 << 10;
           }
         }
+      for (uint32_t ph = 0; ph < NPH; ++ph) {
+        uint32_t h = 0;
+        for (uint32_t l = 0; l < W; ++l) h |= phase_bits(&code[((size_t)ph * W + l) * 4]);
+        for (uint32_t l = 0; l < W; ++l) code[((size_t)ph * W + l) * 4] |= h;
+      }
       uint4* d_code;
       CHECK(hipMalloc(&d_code, code.size() * 4));
       CHECK(hipMemcpy(d_code, code.data(), code.size() * 4, hipMemcpyHostToDevice));
@@ -120,6 +165,13 @@ int main(int argc, char** argv) {
         CHECK(hipEventElapsedTime(&ms, a, b));
         printf("{\"case\": \"vm_%s\", \"W\": %u, \"waves\": %u, \"ms\": %.3f, \"ns_per_phase\": %.1f}\n", names[kind], W,
                grid, ms, ms * 1e6 / NPH);
+        CHECK(hipEventRecord(a));
+        hipLaunchKernelGGL(k_vm_samecode, dim3(grid), dim3(64), 0, 0, d_code, NPH, W, d_cst, d_out);
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        printf("{\"case\": \"vm_%s_samecode\", \"W\": %u, \"waves\": %u, \"ms\": %.3f, \"ns_per_phase\": %.1f}\n",
+               names[kind], W, grid, ms, ms * 1e6 / NPH);
       }
       CHECK(hipFree(d_code));
     }
