@@ -779,6 +779,7 @@ struct ovh_ctx {
   hipEvent_t ev_h[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
+  hipEvent_t ev_vote = nullptr;  // after the latest pipelined vote kernel (batch_front)
   uint32_t* state_slot[OVH_BATCH_SLOTS] = {};
   uint32_t* red_slot[OVH_BATCH_SLOTS] = {};  // fold regions R0..R3 (R1: the 16-vote groups)
   int32_t* grp_ok[OVH_BATCH_SLOTS] = {};
@@ -1048,8 +1049,17 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   uint64_t seed, base;
   CHK(draw_seed(c, &seed, &base));
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
-  {  // hash_to_field right before the vote kernel on the same stream (a cross-stream event
-     // hand-off cost more than the kernel, r02f/r02g kernel traces)
+  if (pipelined) {  // hash_to_field on hstream once the previous vote kernel finished: it runs
+                    // beside that batch's fold levels (a few workgroups) instead of before this
+                    // vote on the main stream, and never beside a vote kernel
+    HIPCHK(hipStreamWaitEvent(c->hstream, c->ev_vote, 0));
+    {
+      StageScope p(c, ST_H2F, c->hstream);
+      k_h2f<<<nblk(n), WG, 0, c->hstream>>>(n, d_hashes, c->xmd, s);
+    }
+    HIPCHK(hipEventRecord(c->ev_h[slot], c->hstream));
+    HIPCHK(hipStreamWaitEvent(st, c->ev_h[slot], 0));
+  } else {
     StageScope p(c, ST_H2F);
     k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s);
   }
@@ -1062,6 +1072,7 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
       k_vm_vote_t<<<nwg, 64, LDS_VOTE_T, st>>>(n, c->vm_vote_t, c->vm_fold, c->vm_consts, key.pts, d_sigs, s, seed,
                                                base, d_codes, region_F(c, slot, 0));
   }
+  if (pipelined) HIPCHK(hipEventRecord(c->ev_vote, st));
   {  // fold level 1: R0 -> R1 (one partial per 16-vote group, kept for the bisection)
     StageScope p(c, ST_FOLD);
     const uint32_t m1 = (nwg + 3) / 4;
@@ -1374,6 +1385,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
          hipEventCreateWithFlags(&c->ev_h[k], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_back[k], hipEventDisableTiming) == hipSuccess;
   for (int k = 0; ok && k < 4; ++k) ok = hipEventCreateWithFlags(&c->ev_x[k], hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->ev_vote, hipEventDisableTiming) == hipSuccess;
   if (ok && (flags & OVH_FLAG_PROFILE))
     for (int k = 0; ok && k < OVH_NSTAGES; ++k)
       ok = hipEventCreate(&c->ev0[k]) == hipSuccess && hipEventCreate(&c->ev1[k]) == hipSuccess;
@@ -1433,6 +1445,7 @@ static void destroy_one(ovh_ctx* c) {
       if (e) (void)hipEventDestroy(e);
   for (int k = 0; k < 4; ++k)
     if (c->ev_x[k]) (void)hipEventDestroy(c->ev_x[k]);
+  if (c->ev_vote) (void)hipEventDestroy(c->ev_vote);
   for (int k = 0; k < OVH_NSTAGES; ++k) {
     if (c->ev0[k]) (void)hipEventDestroy(c->ev0[k]);
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
