@@ -414,9 +414,9 @@ VM_FN void fp_inv(Fp& r, const Fp& a, const Fp& r3) {
   fp_mul(r, x, r3);
 }
 
-// phase header bits (w0 bits 22..28, tools/fpvm/sched.py H_*)
+// phase header bits (w0 bits 22..29, tools/fpvm/sched.py H_*)
 constexpr uint32_t H_MUL = 1u << 22, H_MULNEG = 1u << 23, H_FLAG = 1u << 24, H_LIN = 1u << 25,
-                   H_LINNEG = 1u << 26, H_ACC = 1u << 27, H_RARE = 1u << 28;
+                   H_LINNEG = 1u << 26, H_ACC = 1u << 27, H_RARE = 1u << 28, H_SELB = 1u << 29;
 constexpr uint32_t H_ANY = H_MUL | H_LIN | H_ACC | H_RARE;
 #if defined(__HIPCC__)
 // the header is the same in every lane: read it once into an SGPR
@@ -446,18 +446,26 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
   const uint32_t imm = (in.x >> 16) & 63;
   // four operands, always valid references (a missing one is the zero constant); selb (bit imm
   // of the vote's scalar ? C : B) is a one-term unit lin: A := the picked operand, B = C = 0
-  const bool selb = op == OP_SELB;
-  const bool bit = ((scalar >> imm) & 1) != 0;
-  const uint32_t ra = selb ? (bit ? (in.z & 0xFFFF) : (in.y >> 16)) : (in.y & 0xFFFF);
-  const uint32_t rb = selb ? CONST_BASE + KZERO : in.y >> 16;
-  const uint32_t rc = selb ? CONST_BASE + KZERO : in.z & 0xFFFF;
+  uint32_t ra = in.y & 0xFFFF, rb = in.y >> 16, rc = in.z & 0xFFFF;
+  int ca = ((int)(in.w << 27)) >> 27, cb = ((int)(in.w << 22)) >> 27;
+  int cc = ((int)(in.w << 17)) >> 27, cd = ((int)(in.w << 12)) >> 27;
+  bool selb = false;
+  if (hdr & H_SELB) {
+    selb = op == OP_SELB;
+    const bool bit = ((scalar >> imm) & 1) != 0;
+    ra = selb ? (bit ? rc : rb) : ra;
+    rb = selb ? CONST_BASE + KZERO : rb;
+    rc = selb ? CONST_BASE + KZERO : rc;
+    ca = selb ? 1 : ca;
+    cb = selb ? 0 : cb;
+    cc = selb ? 0 : cc;
+    cd = selb ? 0 : cd;
+  }
   Fp A, B, C, D;
-  ld_slot(A, slots, cst, ra);
-  ld_slot(B, slots, cst, rb);
-  ld_slot(C, slots, cst, rc);
+  ld_slot(B, slots, cst, rb);  // B and D first: the pre-add's negations start with them
   ld_slot(D, slots, cst, in.z >> 16);
-  const int ca = selb ? 1 : ((int)(in.w << 27)) >> 27, cb = selb ? 0 : ((int)(in.w << 22)) >> 27;
-  const int cc = selb ? 0 : ((int)(in.w << 17)) >> 27, cd = selb ? 0 : ((int)(in.w << 12)) >> 27;
+  ld_slot(A, slots, cst, ra);
+  ld_slot(C, slots, cst, rc);
   const bool is_mul = op == OP_MULS || op == OP_SGN0 || op == OP_LEX || op == OP_EQ;
   const bool lin_unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1;
   const bool is_lin = (op == OP_LIN && lin_unit) || selb;

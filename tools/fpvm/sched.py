@@ -355,7 +355,7 @@ def encode(sc):
 
 
 # phase header bits (fpvm.hpp exec): which interpreter blocks any lane of the phase needs
-H_MUL, H_MULNEG, H_FLAG, H_LIN, H_LINNEG, H_ACC, H_RARE = (1 << k for k in range(22, 29))
+H_MUL, H_MULNEG, H_FLAG, H_LIN, H_LINNEG, H_ACC, H_RARE, H_SELB = (1 << k for k in range(22, 30))
 
 
 def phase_bits(w):
@@ -367,7 +367,7 @@ def phase_bits(w):
     if opc in (OPC["muls"], OPC["sgn0"], OPC["lex"], OPC["eq"]):
         return H_MUL | (H_MULNEG if cb < 0 or cd < 0 else 0) | (0 if opc == OPC["muls"] else H_FLAG)
     if opc == OPC["selb"]:
-        return H_LIN
+        return H_LIN | H_SELB
     if opc == OPC["lin"]:
         if ca == 1 and all(-1 <= c <= 1 for c in (cb, cc, cd)):
             return H_LIN | (H_LINNEG if min(cb, cc, cd) < 0 else 0)

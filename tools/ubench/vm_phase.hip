@@ -82,7 +82,7 @@ static uint32_t phase_bits(const uint32_t* w) {
   const int ca = s5(w[3] & 31), cb = s5((w[3] >> 5) & 31), cc = s5((w[3] >> 10) & 31), cd = s5((w[3] >> 15) & 31);
   if (opc == OP_MULS || opc == OP_SGN0 || opc == OP_LEX || opc == OP_EQ)
     return H_MUL | ((cb < 0 || cd < 0) ? H_MULNEG : 0) | (opc == OP_MULS ? 0 : H_FLAG);
-  if (opc == OP_SELB) return H_LIN;
+  if (opc == OP_SELB) return H_LIN | H_SELB;
   if (opc == OP_LIN) {
     const bool unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1;
     return unit ? (H_LIN | ((cb < 0 || cc < 0 || cd < 0) ? H_LINNEG : 0)) : H_ACC;
