@@ -63,6 +63,29 @@ VM_FN void ld_slot(Fp& r, const uint32_t* __restrict__ slots, const uint32_t* __
   r.v[8] = c.x; r.v[9] = c.y; r.v[10] = c.z; r.v[11] = c.w;
 }
 
+VM_FN const uint4* slot_ptr(const uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst, uint32_t ref) {
+  return reinterpret_cast<const uint4*>(((ref & CONST_BASE) ? cst : slots) + (ref & (CONST_BASE - 1)) * 12);
+}
+
+// the four operands of a phase, loaded limb-quarter-major (B, D, A, C for limbs 0..3, then 4..7,
+// then 8..11): the pre-add / lin chains start on the low limbs while the rest is in flight
+VM_FN void ld_slots4(Fp& A, Fp& B, Fp& C, Fp& D, const uint32_t* __restrict__ slots,
+                     const uint32_t* __restrict__ cst, uint32_t ra, uint32_t rb, uint32_t rc, uint32_t rd) {
+  const uint4 *pa = slot_ptr(slots, cst, ra), *pb = slot_ptr(slots, cst, rb), *pc = slot_ptr(slots, cst, rc),
+              *pd = slot_ptr(slots, cst, rd);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const uint4 b = pb[q], d = pd[q], a = pa[q], c = pc[q];
+    B.v[4 * q] = b.x; B.v[4 * q + 1] = b.y; B.v[4 * q + 2] = b.z; B.v[4 * q + 3] = b.w;
+    D.v[4 * q] = d.x; D.v[4 * q + 1] = d.y; D.v[4 * q + 2] = d.z; D.v[4 * q + 3] = d.w;
+    A.v[4 * q] = a.x; A.v[4 * q + 1] = a.y; A.v[4 * q + 2] = a.z; A.v[4 * q + 3] = a.w;
+    C.v[4 * q] = c.x; C.v[4 * q + 1] = c.y; C.v[4 * q + 2] = c.z; C.v[4 * q + 3] = c.w;
+#if defined(__HIPCC__)
+    __builtin_amdgcn_sched_barrier(0);  // keep the quarter order (the scheduler clusters by address)
+#endif
+  }
+}
+
 VM_FN void st_slot(uint32_t* __restrict__ slots, uint32_t dst, const Fp& z) {
   uint4* d4 = reinterpret_cast<uint4*>(slots + dst * 12);
   d4[0] = make_uint4(z.v[0], z.v[1], z.v[2], z.v[3]);
@@ -462,10 +485,7 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
     cd = selb ? 0 : cd;
   }
   Fp A, B, C, D;
-  ld_slot(B, slots, cst, rb);  // B and D first: the pre-add's negations start with them
-  ld_slot(D, slots, cst, in.z >> 16);
-  ld_slot(A, slots, cst, ra);
-  ld_slot(C, slots, cst, rc);
+  ld_slots4(A, B, C, D, slots, cst, ra, rb, rc, in.z >> 16);
   const bool is_mul = op == OP_MULS || op == OP_SGN0 || op == OP_LEX || op == OP_EQ;
   const bool lin_unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1;
   const bool is_lin = (op == OP_LIN && lin_unit) || selb;

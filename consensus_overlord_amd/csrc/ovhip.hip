@@ -180,6 +180,14 @@ struct VmDev {  // a program in device memory
 };
 
 #define VM_SLICES 4  // 16-lane slices per 64-lane workgroup (vote, vote_t)
+// LDS layout of the VM kernels (words): the constant table, then slot regions that start on a
+// 128-byte boundary and repeat at 128-byte strides, so slot s and constant c share LDS banks
+// exactly when s = c (mod 8) -- the rule tools/fpvm/sched.py spreads operand reads by.
+constexpr uint32_t align128w(uint32_t w) { return (w + 31) / 32 * 32; }
+constexpr uint32_t SLOT_BASE_W = align128w(VM_NCONST * 12);
+constexpr uint32_t VOTE_STRIDE_W = align128w(VM_VOTE_NSLOTS * 12 + 4);  // + 4 header words
+constexpr uint32_t VOTE_T_STRIDE_W = align128w(VM_VOTE_T_NSLOTS * 12 + 4);
+constexpr uint32_t FOLD_STRIDE_W = align128w(VM_FOLD_NSLOTS * 12);
 #define VM_FOLD_UNITS (64 / VM_FOLD_W)  // fold units per 64-lane workgroup
 
 __device__ __forceinline__ void load_consts(uint32_t* cst, const uint32_t* __restrict__ g, uint32_t n) {
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
   const uint32_t slice = threadIdx.x / VM_VOTE_W, lane = threadIdx.x % VM_VOTE_W;
-  uint32_t* slots = lds + VM_NCONST * 12 + slice * (VM_VOTE_NSLOTS * 12 + 4);
+  uint32_t* slots = lds + SLOT_BASE_W + slice * VOTE_STRIDE_W;
   uint32_t* hdr = slots + VM_VOTE_NSLOTS * 12;  // [pflags, code]
   const uint32_t i = blockIdx.x * VM_SLICES + slice;
   const bool active = i < n;
@@ -321,7 +329,7 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
   // and codes are made visible to the workgroup first; the fold reuses the vote slots' LDS.
   __threadfence();
   __syncthreads();
-  fold_unit(blockIdx.x, n, fold, cst, lds + VM_NCONST * 12, threadIdx.x % VM_FOLD_W,
+  fold_unit(blockIdx.x, n, fold, cst, lds + SLOT_BASE_W, threadIdx.x % VM_FOLD_W,
             threadIdx.x < VM_FOLD_W && 4 * blockIdx.x < n,
             Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{s.p + (size_t)S_RS * 12 * s.cap, s.cap}, part0,
             codes);
@@ -338,7 +346,7 @@ __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const ui
   uint32_t* cst = lds;
   const uint32_t slice = threadIdx.x / VM_FOLD_W, lane = threadIdx.x % VM_FOLD_W;
   const uint32_t sl = slice < SLICES ? slice : 0;  // idle slices address slice 0 (never write)
-  uint32_t* slots = lds + VM_NCONST * 12 + sl * VM_FOLD_NSLOTS * 12;
+  uint32_t* slots = lds + SLOT_BASE_W + sl * FOLD_STRIDE_W;
   const uint32_t t = blockIdx.x * SLICES + slice;
   const bool active = slice < SLICES && 4 * t < m;
   load_consts(cst, cst_g, VM_NCONST);
@@ -355,7 +363,7 @@ __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const u
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
-  uint32_t* slots = lds + VM_NCONST * 12;
+  uint32_t* slots = lds + SLOT_BASE_W;
   const uint32_t lane = threadIdx.x;
   load_consts(cst, cst_g, VM_NCONST);
   for (uint32_t k = lane; k < 4 * PART_PLANES; k += 64) {
@@ -399,7 +407,7 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
   const uint32_t slice = threadIdx.x / VM_VOTE_T_W, lane = threadIdx.x % VM_VOTE_T_W;
-  uint32_t* slots = lds + VM_NCONST * 12 + slice * (VM_VOTE_T_NSLOTS * 12 + 4);
+  uint32_t* slots = lds + SLOT_BASE_W + slice * VOTE_T_STRIDE_W;
   uint32_t* hdr = slots + VM_VOTE_T_NSLOTS * 12;  // [sig flags, pk flags]
   const uint32_t i = blockIdx.x * VM_SLICES + slice;
   const bool active = i < n;
@@ -447,7 +455,7 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
   }
   __threadfence();
   __syncthreads();
-  fold_unit(blockIdx.x, n, fold, cst, lds + VM_NCONST * 12, threadIdx.x % VM_FOLD_W,
+  fold_unit(blockIdx.x, n, fold, cst, lds + SLOT_BASE_W, threadIdx.x % VM_FOLD_W,
             threadIdx.x < VM_FOLD_W && 4 * blockIdx.x < n,
             Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{s.p + (size_t)S_RS * 12 * s.cap, s.cap}, part0,
             codes);
@@ -460,7 +468,7 @@ __device__ __forceinline__ bool final_one(uint32_t u, const VmDev& prog, const u
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
-  uint32_t* slots = lds + VM_NCONST * 12;
+  uint32_t* slots = lds + SLOT_BASE_W;
   const uint32_t lane = threadIdx.x;
   load_consts(cst, cst_g, VM_NCONST);
   for (uint32_t k = lane; k < 4 * PART_PLANES; k += 64) {
@@ -806,6 +814,8 @@ struct ovh_ctx {
   ValidatorTable tab;
   uint32_t* qc_buf = nullptr;  // QC batch: apk planes + flags
   uint32_t qc_cap = 0;
+  uint32_t* qt_buf = nullptr;  // explicit-key QC (ovh_verify_aggregated): decoded keys + flags
+  uint32_t qt_cap = 0;
   VerdictCache cache;
   // multi-device (ovh_create_multi): sub-contexts, one per device; the root owns no streams
   std::vector<ovh_ctx*> sub;
@@ -834,21 +844,20 @@ struct ovh_ctx {
 static const char* const STAGE_NAMES[OVH_NSTAGES] = {"hash_to_field", "vote", "fold", "final", "bisect"};
 
 // LDS bytes of the VM kernels: constants + slices x slots (+ a 16-byte slice header for vote)
-static constexpr size_t LDS_VOTE = (size_t)VM_NCONST * 48 + VM_SLICES * ((size_t)VM_VOTE_NSLOTS * 48 + 16);
-static constexpr size_t LDS_VOTE_T = (size_t)VM_NCONST * 48 + VM_SLICES * ((size_t)VM_VOTE_T_NSLOTS * 48 + 16);
-static constexpr size_t LDS_FOLD = (size_t)VM_NCONST * 48 + VM_FOLD_UNITS * (size_t)VM_FOLD_NSLOTS * 48;
-static constexpr size_t LDS_FINAL = (size_t)VM_NCONST * 48 + (size_t)VM_FINAL_NSLOTS * 48;
+static constexpr size_t LDS_VOTE = ((size_t)SLOT_BASE_W + VM_SLICES * (size_t)VOTE_STRIDE_W) * 4;
+static constexpr size_t LDS_VOTE_T = ((size_t)SLOT_BASE_W + VM_SLICES * (size_t)VOTE_T_STRIDE_W) * 4;
+static constexpr size_t LDS_FOLD = ((size_t)SLOT_BASE_W + VM_FOLD_UNITS * (size_t)FOLD_STRIDE_W) * 4;
+static constexpr size_t LDS_FINAL = ((size_t)SLOT_BASE_W + (size_t)VM_FINAL_NSLOTS * 12) * 4;
 static_assert(VM_VOTE_W * VM_SLICES == 64 && VM_VOTE_T_W * VM_SLICES == 64 && VM_FOLD_W * VM_FOLD_UNITS == 64 &&
                   VM_FINAL_W == 64, "VM slice widths");
-static constexpr size_t LDS_FOLD1 = (size_t)VM_NCONST * 48 + (size_t)VM_FOLD_NSLOTS * 48;
+static constexpr size_t LDS_FOLD1 = ((size_t)SLOT_BASE_W + (size_t)FOLD_STRIDE_W) * 4;
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
 // allocation granules assumed)
 constexpr size_t lds_granule(size_t b) { return (b + 1023) / 1024 * 1024; }
 static_assert(4 * lds_granule(LDS_VOTE > LDS_VOTE_T ? LDS_VOTE : LDS_VOTE_T) + 2 * lds_granule(LDS_FINAL) <= 160 * 1024,
               "four vote workgroups + two finals per CU");
-static_assert(VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_NSLOTS * 12 + 4) &&
-                  VM_FOLD_NSLOTS * 12 <= VM_SLICES * (VM_VOTE_T_NSLOTS * 12 + 4),
+static_assert(FOLD_STRIDE_W <= VM_SLICES * VOTE_STRIDE_W && FOLD_STRIDE_W <= VM_SLICES * VOTE_T_STRIDE_W,
               "fused fold reuses the vote slots");
 
 static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphases, uint32_t W, uint32_t NW,
@@ -1437,7 +1446,8 @@ static void destroy_one(ovh_ctx* c) {
       if (p) (void)hipFree(p);
   for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vm_consts,
                   (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
-                  (void*)c->tab.planes, (void*)c->tab.flags, (void*)c->qc_buf, (void*)c->gather, (void*)c->mfin})
+                  (void*)c->tab.planes, (void*)c->tab.flags, (void*)c->qc_buf, (void*)c->qt_buf, (void*)c->gather,
+                  (void*)c->mfin})
     if (p) (void)hipFree(p);
   for (void* p : c->vm_bufs) (void)hipFree(p);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
@@ -1716,9 +1726,88 @@ int ovh_aggregate_pks(ovh_ctx* c, const uint8_t* pks, const size_t* pk_lens, siz
   return sum_pks(c, pks, pk_lens, n, 0, out, &sum);
 }
 
+static int ensure_qc_buf(ovh_ctx* c, size_t nd) {
+  if (nd <= c->qc_cap && c->qc_buf) return 0;
+  if (c->qc_buf) (void)hipFree(c->qc_buf);
+  c->qc_buf = nullptr;
+  c->qc_cap = 0;
+  uint32_t cap = 64;
+  while (cap < nd) cap <<= 1;
+  HIPCHK(hipMalloc(&c->qc_buf, (size_t)(3 * 12 + 1) * cap * 4));
+  c->qc_cap = cap;
+  return 0;
+}
+
+// verify_aggregated_signature (consensus.rs:365-382) on the batch kernels: the keys decoded and
+// group-checked lane by lane (k_table_build), their sum (k_qc_apk), then the vote_t program and
+// the final check for the one (sig, hash, apk). Returns 1 when the exact one-lane path must
+// decide instead (a key outside G1: the sum's own group check decides; other encodings).
+static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, const uint8_t* hash,
+                                size_t hash_len, const uint8_t* pks, const size_t* pk_lens, size_t n, int* code) {
+  if (n == 0 || agg_len != 96 || !hash || hash_len != 32) return 1;
+  for (size_t i = 0; i < n; ++i)
+    if (pk_lens[i] != 48) return 1;
+  if (n > c->qt_cap || !c->qt_buf) {
+    if (c->qt_buf) (void)hipFree(c->qt_buf);
+    c->qt_buf = nullptr;
+    c->qt_cap = 0;
+    uint32_t cap = 64;
+    while (cap < n) cap <<= 1;
+    HIPCHK(hipMalloc(&c->qt_buf, (size_t)(3 * 12 + 1) * cap * 4));
+    c->qt_cap = cap;
+  }
+  CHK(ensure_qc_buf(c, 1));
+  CHK(ensure_in(c, n * 48 + 96 + 32 + 64 + 8 * (n + 1)));
+  uint8_t* d = c->in_buf;  // keys | sig | hash | code | off[2] | ent[n]
+  int32_t* dc = (int32_t*)(d + ((n * 48 + 128 + 15) & ~(size_t)15));
+  uint32_t* doff = (uint32_t*)(dc + 4);
+  uint32_t* dent = doff + 2;
+  std::vector<uint32_t> hv(2 + n);
+  hv[0] = 0;
+  hv[1] = (uint32_t)n;
+  for (size_t i = 0; i < n; ++i) hv[2 + i] = (uint32_t)i;
+  HIPCHK(hipMemcpyAsync(d, pks, n * 48, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(d + n * 48, agg_sig, 96, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(d + n * 48 + 96, hash, 32, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(doff, hv.data(), hv.size() * 4, hipMemcpyHostToDevice, c->stream));
+  uint32_t* kflags = c->qt_buf + (size_t)3 * 12 * c->qt_cap;
+  k_table_build<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, d, Slab{c->qt_buf, c->qt_cap}, kflags);
+  HIPCHK(hipGetLastError());
+  std::vector<uint32_t> hf(n);
+  HIPCHK(hipMemcpyAsync(hf.data(), kflags, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  uint32_t fl = 0;
+  for (size_t i = 0; i < n; ++i) fl |= hf[i];
+  // consensus.rs:454-458 order as sum_pks: any unparsable key -> "lose public key"
+  if (fl & PKF_PARSE) {
+    *code = OVH_ERR_PUBKEY;
+    return 0;
+  }
+  if (fl & PKF_GRP) return 1;
+  uint32_t* qflags = c->qc_buf + (size_t)3 * 12 * c->qc_cap;
+  k_qc_apk<<<1, WG, 0, c->stream>>>(1, doff, dent, Slab{c->qt_buf, c->qt_cap}, Slab{c->qc_buf, c->qc_cap}, qflags);
+  HIPCHK(hipGetLastError());
+  CHK(ensure_cap(c, 1));
+  CHK(verify_async_locked(c, 1, d + n * 48, d + n * 48 + 96, KeySrc{nullptr, PkSrc{c->qc_buf, c->qc_cap, qflags, nullptr}},
+                          dc));
+  CHK(sync_all(c));
+  int32_t r = -1;
+  HIPCHK(hipMemcpyAsync(&r, dc, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  *code = r;
+  return 0;
+}
+
 static int verify_aggregated_locked(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, const uint8_t* hash,
-                                    size_t hash_len, const uint8_t* pks, const size_t* pk_lens, size_t n) {
+                                    size_t hash_len, const uint8_t* pks, const size_t* pk_lens, size_t n,
+                                    bool exact = false) {
   HIPCHK(hipSetDevice(c->device));
+  if (!exact) {
+    int code = 0;
+    const int r = verify_aggregated_vm(c, agg_sig, agg_len, hash, hash_len, pks, pk_lens, n, &code);
+    if (r < 0 || r >= OVH_ERR_ARG) return r;
+    if (r == 0) return code;
+  }
   uint32_t* sum = nullptr;
   CHK(sum_pks(c, pks, pk_lens, n, 1024 + agg_len, nullptr, &sum));
   // stage sig + hash behind the sum (sum occupies 36 words + 48 bytes)
@@ -1875,7 +1964,8 @@ static int qc_batch_locked(ovh_ctx* c, size_t nq, const uint8_t* sigs, const uin
         lens.push_back(48);
       }
       ent.resize(start);
-      const int r = verify_aggregated_locked(c, sigs + 96 * q, 96, hashes + 32 * q, 32, cat.data(), lens.data(), cnt);
+      const int r =
+          verify_aggregated_locked(c, sigs + 96 * q, 96, hashes + 32 * q, 32, cat.data(), lens.data(), cnt, true);
       if (r >= OVH_ERR_ARG) return r;
       codes[q] = r;
     } else {
@@ -1886,15 +1976,7 @@ static int qc_batch_locked(ovh_ctx* c, size_t nq, const uint8_t* sigs, const uin
   const size_t nd = dev.size();
   if (!nd) return 0;
   // device batch: apk per QC -> vote_t over (sig, hash, apk)
-  if (nd > c->qc_cap || !c->qc_buf) {
-    if (c->qc_buf) (void)hipFree(c->qc_buf);
-    c->qc_buf = nullptr;
-    c->qc_cap = 0;
-    uint32_t cap = 64;
-    while (cap < nd) cap <<= 1;
-    HIPCHK(hipMalloc(&c->qc_buf, (size_t)(3 * 12 + 1) * cap * 4));
-    c->qc_cap = cap;
-  }
+  CHK(ensure_qc_buf(c, nd));
   const size_t bytes = nd * (96 + 32 + 4) + off.size() * 4 + ent.size() * 4 + 256;
   CHK(ensure_in(c, bytes));
   uint8_t* d = c->in_buf;

@@ -20,6 +20,7 @@ Instruction (4 x uint32 per lane per phase):
 from __future__ import annotations
 
 import heapq
+import os
 from collections import defaultdict
 
 from ir import CMAX, HALF_P, HEAVY, P, lin_form
@@ -28,6 +29,8 @@ OPC = {"nop": 0, "muls": 1, "sgn0": 2, "lex": 3, "inv": 4, "lin": 5, "sel": 6, "
        "xor": 10, "st": 11, "selb": 12, "sop": 13}
 CONST_BASE = 0x800
 ABSENT = 0xFFFF
+# LDS pass width (lanes) and slot residues that share banks (OVH_BANK="lanes,mod" for A/B builds)
+BANK_LANES, BANK_MOD = (int(x) for x in os.environ.get("OVH_BANK", "16,16").split(","))
 R_MONT = pow(2, 384, P)
 
 
@@ -213,14 +216,50 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
     free = []
     nslots = 0
     frees_at = defaultdict(list)   # round -> slots that become free at that round
+    # LDS bank spreading: a ds_read_b128 / ds_write_b128 serves BANK_LANES lanes per pass, and two
+    # lanes of a pass that touch different addresses with the same 16-byte chunk residue hit the
+    # same banks. Slot regions are 128-byte aligned (ovhip.hip), so slot s and constant c sit in
+    # residues 3 s and 3 c (mod 8): equal iff s = c (mod BANK_MOD). Among the free slots a value
+    # gets the one whose residue the fewest distinct addresses use in the same instruction (phase,
+    # operand position, lane pass) where it is read or written; the slot count is unchanged (a
+    # new slot only when none is free).
+    for i in pre:
+        if ops[i].kind == "const":
+            consts.ref(ops[i].imm, ops[i].name == "raw")
+    zero_c = consts.ref(0, False) - CONST_BASE
+    lane_of = {}
+    reads = defaultdict(set)
+    use = defaultdict(lambda: [0] * BANK_MOD)
+    seen_c = set()
+    for t, r in enumerate(rounds):
+        for k, i in enumerate(r):
+            lane_of[i] = k
+            g = k // BANK_LANES
+            A, B, C, D = lane_operands(prog, i)[:4]
+            refs = [(0, B), (0, C)] if ops[i].kind == "selb" else list(enumerate((A, B, C, D)))
+            for pos, v in refs:
+                if v is not None and ops[v].kind != "const":
+                    reads[v].add((t, g, pos))
+                    continue
+                c = zero_c if v is None else consts.ref(ops[v].imm, ops[v].name == "raw") - CONST_BASE
+                if (t, g, pos, c) not in seen_c:
+                    seen_c.add((t, g, pos, c))
+                    use[(t, g, pos)][c % BANK_MOD] += 1
 
     def alloc(v):
         nonlocal nslots
+        ev = [use[e] for e in reads[v]]
+        if v in lane_of:
+            ev.append(use[(def_round[v], lane_of[v] // BANK_LANES, "w")])
         if free:
-            s = heapq.heappop(free)
+            best = min(free, key=lambda x: (sum(u[x % BANK_MOD] for u in ev), x))
+            free.remove(best)
+            s = best
         else:
             s = nslots
             nslots += 1
+        for u in ev:
+            u[s % BANK_MOD] += 1
         slot_of[v] = s
         lu = last_use[v]
         if lu < 0:   # never read (dead write): free right after
@@ -231,8 +270,7 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
         if v in liveset:
             alloc(v)
     for t, r in enumerate(rounds):
-        for s in frees_at.pop(t, []):
-            heapq.heappush(free, s)
+        free.extend(frees_at.pop(t, []))
         for i in r:
             if ops[i].kind != "st":
                 alloc(i)
@@ -268,6 +306,68 @@ def words_per_lane(prog):
     return 4
 
 
+def lane_operands(prog, i):
+    """(A, B, C, D, coefs, scale) of op i as the interpreter reads them (value ids or None:
+    None is the zero constant; C of sgn0 / lex / eq / inv is a fixed constant, see encode)."""
+    ops = prog.ops
+    LW = prog.lin_width
+    op = ops[i]
+    k = op.kind
+    s = list(op.srcs) + [None] * (LW - len(op.srcs))
+    coefs = [0] * LW
+    ext = [None] * 4          # operands E..H (wide programs)
+    scale = 0
+    if k == "lin":
+        form = lin_form(prog._lin_terms(op), LW)
+        if form[0] == "acc":
+            srcs = list(op.srcs) + [None] * (LW - len(op.srcs))
+            coefs = list(op.coefs) + [0] * (LW - len(op.coefs))
+        else:
+            u = form[-1] + [(0, None)] * (LW - len(form[-1]))
+            srcs = [v for _, v in u]
+            coefs = [c for c, _ in u]
+            if form[0] == "scaled":
+                scale = form[1]
+        A, B, C, D = srcs[:4]
+        if LW == 8:
+            ext = srcs[4:8]
+    elif k == "eq":            # (A - B) * plain 1, flag: zero (fpvm.hpp exec)
+        assert tuple(op.coefs[:4]) == (1, 0, 1, 0) and s[1] is None and s[3] is None, op.coefs
+        A, B, C, D = s[0], s[2], None, None
+        coefs[:4] = [1, -1, 1, 0]
+    elif k == "muls":
+        A, B, C, D = s[:4]
+        coefs[:4] = list(op.coefs[:4])
+        for h in (0, 2):
+            terms = [(c, v) for c, v in zip(op.coefs[h:h + 2], s[h:h + 2]) if v is not None and c]
+            form = lin_form(terms, 2)
+            assert form[0] == "unit", (k, op.coefs)   # the interpreter's muls operands are unit sums
+            u = form[1] + [(0, None)] * (2 - len(form[1]))
+            if h == 0:
+                A, B = u[0][1], u[1][1]
+            else:
+                C, D = u[0][1], u[1][1]
+            coefs[h], coefs[h + 1] = u[0][0], u[1][0]
+    elif k == "sop":           # A C + cb B D
+        A, B, C, D = s[:4]
+        coefs[:4] = list(op.coefs[:4])
+    elif k in ("sgn0", "lex"):
+        A, B, C, D = s[0], None, None, None
+        coefs[:4] = [1, 0, 1, 0]
+    elif k in ("inv", "st"):
+        A, B, C, D = s[0], None, None, None
+        coefs[:4] = [1, 0, 0, 0]
+    elif k == "sel":           # A = flag, B = x, C = y
+        A, B, C, D = s[0], s[1], s[2], None
+    elif k == "selb":          # B = x, C = y
+        A, B, C, D = None, s[0], s[1], None
+    elif k in ("and", "or", "xor"):
+        A, B, C, D = s[0], None, s[1], None
+    else:
+        raise ValueError(k)
+    return A, B, C, D, coefs, scale
+
+
 def encode(sc):
     """-> list of uint32 words, nphases * W * words_per_lane."""
     words = []
@@ -282,58 +382,7 @@ def encode(sc):
                 continue
             op = ops[i]
             k = op.kind
-            s = list(op.srcs) + [None] * (LW - len(op.srcs))
-            coefs = [0] * LW
-            ext = [None] * 4          # operands E..H (wide programs)
-            scale = 0
-            if k == "lin":
-                form = lin_form(sc.prog._lin_terms(op), LW)
-                if form[0] == "acc":
-                    srcs = list(op.srcs) + [None] * (LW - len(op.srcs))
-                    coefs = list(op.coefs) + [0] * (LW - len(op.coefs))
-                else:
-                    u = form[-1] + [(0, None)] * (LW - len(form[-1]))
-                    srcs = [v for _, v in u]
-                    coefs = [c for c, _ in u]
-                    if form[0] == "scaled":
-                        scale = form[1]
-                A, B, C, D = srcs[:4]
-                if LW == 8:
-                    ext = srcs[4:8]
-            elif k == "eq":            # (A - B) * plain 1, flag: zero (fpvm.hpp exec)
-                assert tuple(op.coefs[:4]) == (1, 0, 1, 0) and s[1] is None and s[3] is None, op.coefs
-                A, B, C, D = s[0], s[2], None, None
-                coefs[:4] = [1, -1, 1, 0]
-            elif k == "muls":
-                A, B, C, D = s[:4]
-                coefs[:4] = list(op.coefs[:4])
-                for h in (0, 2):
-                    terms = [(c, v) for c, v in zip(op.coefs[h:h + 2], s[h:h + 2]) if v is not None and c]
-                    form = lin_form(terms, 2)
-                    assert form[0] == "unit", (k, op.coefs)   # the interpreter's muls operands are unit sums
-                    u = form[1] + [(0, None)] * (2 - len(form[1]))
-                    if h == 0:
-                        A, B = u[0][1], u[1][1]
-                    else:
-                        C, D = u[0][1], u[1][1]
-                    coefs[h], coefs[h + 1] = u[0][0], u[1][0]
-            elif k == "sop":           # A C + cb B D
-                A, B, C, D = s[:4]
-                coefs[:4] = list(op.coefs[:4])
-            elif k in ("sgn0", "lex"):
-                A, B, C, D = s[0], None, None, None
-                coefs[:4] = [1, 0, 1, 0]
-            elif k in ("inv", "st"):
-                A, B, C, D = s[0], None, None, None
-                coefs[:4] = [1, 0, 0, 0]
-            elif k == "sel":           # A = flag, B = x, C = y
-                A, B, C, D = s[0], s[1], s[2], None
-            elif k == "selb":          # B = x, C = y
-                A, B, C, D = None, s[0], s[1], None
-            elif k in ("and", "or", "xor"):
-                A, B, C, D = s[0], None, s[1], None
-            else:
-                raise ValueError(k)
+            A, B, C, D, coefs, scale = lane_operands(sc.prog, i)
             dst = sc.slot_of.get(i, 0)
             w0 = OPC[k] | dst << 5 | (op.imm & 63) << 16
             if k in ("sgn0", "lex", "eq"):
