@@ -5,7 +5,7 @@
 #include <stdio.h>
 
 #include "../../consensus_overlord_amd/csrc/bls/fp.hpp"
-#include "../../consensus_overlord_amd/csrc/bls/fp_mul2_gfx950.hpp"
+#include "fp_mul2_gfx950.hpp"
 
 using namespace ovh;
 
