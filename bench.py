@@ -53,7 +53,7 @@ W_V_CANON = 18300   # algorithmic Montgomery products per verifi
 STAGE_TO_WORK = {"hash_to_field": "hash_to_field", "vote": "vote", "fold": "fold_per_partial",
                  "final": "final_per_batch", "fallback": "fallback"}
 PER_BATCH_STAGES = {"final"}
-NSTAGES = 5
+NSTAGES = 6
 
 
 def synth_inputs(lib, lo: int, n: int):

@@ -3,16 +3,19 @@
 // Batch verification (ovh_verify_batch_device), DESIGN.md section 4:
 //   k_h2f         lane per vote: expand_message_xmd (SHA-256) + hash_to_field -> u0, u1
 //   k_vm_vote     16-lane slice per vote, 4 votes per wave: the Fp-VM "vote" program --
-//                 pk / sig decompression + subgroup checks, hash_to_G2, r pk, r sigma,
-//                 f = Miller(r pk, H); the epilogue writes the vote's code with the reference
-//                 precedence and its (f, r sigma) contribution (identity if the vote failed),
-//                 then folds the workgroup's 4 votes into one partial (level 0)
+//                 pk / sig decompression + subgroup checks, hash_to_G2, r pk,
+//                 f = Miller(r pk, H), sigma and tau = -psi^2(sigma) stored for the MSM; the
+//                 epilogue writes the vote's code with the reference precedence, then folds
+//                 the workgroup's 4 votes' f into one partial (level 0; 1 if the vote failed)
 //   k_vm_vote_t   the same with the public key from the device validator table (or a QC's
 //                 aggregated key): no decompression / subgroup check of the key
 //   k_vm_fold     fold levels: 4 partials -> (prod f, sum S); level 1 = groups of 16 votes
-//   k_vm_final    one wave: prod f * Miller(-G1, sum S) -> final exponentiation == 1 ?
-//   k_vm_group    bisection, when the combined check failed: the same check per 16-vote group
-//   k_vm_votechk  bisection, per vote of a failing group: f_i * Miller(-G1, r_i sigma_i) == 1
+//   k_msm_*       Pippenger MSM of S = sum r_i sigma_i (msm.hpp), on the final stream
+//   k_vm_final    one wave: prod f * Miller(-G1, S) -> final exponentiation == 1 ?
+//   bisection, only when the combined check failed (device-gated):
+//   k_vm_rs       per vote r_i sigma_i (the MSM's terms), then fold levels 0-1 of (f, r sigma)
+//   k_vm_group    the same check per 16-vote group
+//   k_vm_votechk  per vote of a failing group: f_i * Miller(-G1, r_i sigma_i) == 1
 // Per-vote state lives in HBM as structure-of-arrays by limb: limb k of element i of an Fp
 // plane j at slab[(j * 12 + k) * cap + i].
 #include <hip/hip_runtime.h>
@@ -104,8 +107,10 @@ struct Slab {
 // Fp planes of the per-vote state slab.
 enum : uint32_t {
   S_U = VM_S_U,       // 4 planes: u0, u1 (hash_to_field, Montgomery)
-  S_RS = VM_S_RS,     // 6 planes: r * sig (projective)
+  S_SIG = VM_S_SIG,   // 4 planes: sigma (affine)
+  S_TAU = VM_S_TAU,   // 4 planes: tau = -psi^2(sigma) (affine)
   S_F = VM_S_F,       // 12 planes: f = Miller(r pk, H)
+  S_RS = VM_S_RS,     // 6 planes: r * sig (projective; bisection only, k_vm_rs)
   S_TOTAL = VM_S_TOTAL,
 };
 // partial = (F: 12 planes, S: 6 planes)
@@ -113,8 +118,8 @@ constexpr uint32_t PART_PLANES = 18;
 // words per fin region: 16 unpacked + 4 folded partials as planes
 constexpr size_t FIN_STRIDE = (size_t)PART_PLANES * 12 * 20;
 
-enum : int { ST_H2F = 0, ST_VOTE, ST_FOLD, ST_FINAL, ST_FALLBACK };
-static_assert(ST_FALLBACK + 1 == OVH_NSTAGES, "stage table");
+enum : int { ST_H2F = 0, ST_VOTE, ST_FOLD, ST_FINAL, ST_FALLBACK, ST_MSM };
+static_assert(ST_MSM + 1 == OVH_NSTAGES, "stage table");
 
 __device__ __forceinline__ uint64_t rlc_scalar(uint64_t seed, uint64_t i) {
   // SplitMix64 on (seed, i): the 64-bit RLC coefficient of vote i (never 0). The seed is a
@@ -209,6 +214,7 @@ __device__ __forceinline__ uint32_t slot_flag_get(const uint32_t* slots, uint32_
 
 // One fold unit on a 16-lane slice: out[t] = (prod F, sum S) over in[4t .. 4t+3] (missing ->
 // identity); with codes (level 0) every vote whose code is not 0 contributes the identity.
+// inS.p null: every S is the identity (the batch path's S is the MSM's, msm.hpp).
 // All 64 threads of the workgroup call it (the phase barrier); `active` marks the working slice.
 __device__ __forceinline__ void fold_unit(uint32_t t, uint32_t m, const VmDev& prog, const uint32_t* cst,
                                           uint32_t* slots, uint32_t lane, bool active, Slab inF, Slab inS,
@@ -217,7 +223,7 @@ __device__ __forceinline__ void fold_unit(uint32_t t, uint32_t m, const VmDev& p
     for (uint32_t k = lane; k < 4 * PART_PLANES; k += VM_FOLD_W) {
       const uint32_t q = k / PART_PLANES, j = k % PART_PLANES, e = 4 * t + q;
       Fp v;
-      if (e < m && (!codes || codes[e] == 0)) {
+      if (e < m && (!codes || codes[e] == 0) && (j < 12 || inS.p)) {
         if (j < 12) inF.ld(v, j, e);
         else inS.ld(v, j - 12, e);
       } else if (j == 0 || j == 12 + 2) {
@@ -257,8 +263,8 @@ __device__ __forceinline__ void vote_stagger() {
 #endif
 }
 
-// Per vote: VM "vote" program + reference-precedence code + the vote's (f, r sigma)
-// contribution. LDS: constants, then VM_SLICES x (VM_VOTE_NSLOTS slots).
+// Per vote: VM "vote" program + reference-precedence code + the vote's f contribution (its
+// sigma / tau planes feed the MSM). LDS: constants, then VM_SLICES x (VM_VOTE_NSLOTS slots).
 __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
                                                 const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
                                                 Slab s, uint64_t seed, uint64_t base, int32_t* __restrict__ codes,
@@ -331,15 +337,17 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
   __syncthreads();
   fold_unit(blockIdx.x, n, fold, cst, lds + SLOT_BASE_W, threadIdx.x % VM_FOLD_W,
             threadIdx.x < VM_FOLD_W && 4 * blockIdx.x < n,
-            Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{s.p + (size_t)S_RS * 12 * s.cap, s.cap}, part0,
-            codes);
+            Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{nullptr, 0}, part0, codes);
 }
 
 // Fold level: SLICES units per 64-thread workgroup (4 on the main stream; 1 on the final
 // stream, whose 10.8 KB of LDS fits beside a CU's four vote workgroups).
+// gate: skip when *gate == 1 (the bisection's refold after a passed combined check)
 template <int SLICES>
 __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
-                                                Slab inS, Slab out, const int32_t* __restrict__ codes) {
+                                                Slab inS, Slab out, const int32_t* __restrict__ codes,
+                                                const int32_t* __restrict__ gate = nullptr) {
+  if (gate && *gate == 1) return;
   __builtin_amdgcn_s_setprio(2);  // short: run ahead of a co-resident final wave
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
@@ -354,11 +362,12 @@ __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const ui
 }
 
 // Final: prod F * Miller(-G1, sum S) over in[0..m-1] (m <= 4) -> FE == 1 -> *result.
+// xS.p: partial 0's S is xS[0] (the batch's MSM result; the folded partials carry S = O).
 #ifndef OVH_FINAL_PRIO
 #define OVH_FINAL_PRIO 0
 #endif
 __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
-                                                 Slab inS, int32_t* __restrict__ result) {
+                                                 Slab inS, Slab xS, int32_t* __restrict__ result) {
   if (OVH_FINAL_PRIO) __builtin_amdgcn_s_setprio(OVH_FINAL_PRIO);
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
@@ -369,7 +378,9 @@ __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const u
   for (uint32_t k = lane; k < 4 * PART_PLANES; k += 64) {
     const uint32_t q = k / PART_PLANES, j = k % PART_PLANES;
     Fp v;
-    if (q < m) {
+    if (q == 0 && j >= 12 && xS.p) {
+      xS.ld(v, j - 12, 0);
+    } else if (q < m) {
       if (j < 12) inF.ld(v, j, q);
       else inS.ld(v, j - 12, q);
     } else if (j == 0 || j == 12 + 2) {
@@ -457,8 +468,7 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
   __syncthreads();
   fold_unit(blockIdx.x, n, fold, cst, lds + SLOT_BASE_W, threadIdx.x % VM_FOLD_W,
             threadIdx.x < VM_FOLD_W && 4 * blockIdx.x < n,
-            Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{s.p + (size_t)S_RS * 12 * s.cap, s.cap}, part0,
-            codes);
+            Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{nullptr, 0}, part0, codes);
 }
 
 // The final program on one unit given as (F planes, S planes) at index u (the other three
@@ -515,6 +525,34 @@ __global__ __launch_bounds__(64) void k_vm_votechk(uint32_t n, VmDev prog, const
                             Slab{s.p + (size_t)S_RS * 12 * s.cap, s.cap});
   if (threadIdx.x == 0) codes[i] = ok ? 0 : BLST_VERIFY_FAIL;
 }
+
+// Bisection, first step (skipped when *verdict == 1): r_i sigma_i of every vote with code 0 from
+// its stored sigma / tau (program "rs", the vote's RLC value) -> S_RS planes, for the group and
+// per-vote checks (the batch path sums these terms by the MSM instead).
+constexpr uint32_t RS_STRIDE_W = align128w(VM_RS_NSLOTS * 12);
+__global__ __launch_bounds__(64) void k_vm_rs(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g, Slab s,
+                                              uint64_t seed, uint64_t base, const int32_t* __restrict__ codes,
+                                              const int32_t* __restrict__ verdict) {
+  if (verdict && *verdict == 1) return;
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / VM_RS_W, lane = threadIdx.x % VM_RS_W;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * RS_STRIDE_W;
+  const uint32_t i = blockIdx.x * (64 / VM_RS_W) + slice;
+  const bool active = i < n && codes[i] == 0;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active && lane < VM_RS_NIN) {
+    Fp v;
+    s.ld(v, (lane < 4 ? S_SIG : S_TAU - 4) + lane, i);
+    slot_put(slots, VM_RS_IN[lane], v.v);
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_RS_NPHASES, VM_RS_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
+          vm::Out{s.p, s.cap, i});
+}
+
+#include "msm.hpp"
 
 // Validator table (ovh_set_validators): lane per key, 48-byte compressed -> flags + the point
 // (X : Y : Z) Montgomery, (0 : 1 : 0) for infinity or a failed parse.
@@ -822,8 +860,12 @@ struct ovh_ctx {
   std::atomic<uint32_t> rr{0};
   uint8_t* gather = nullptr;  // on sub[0]'s device: ndev x 864 B
   uint32_t* mfin = nullptr;   // on sub[0]'s device: unpack scratch of the gathered partials
+  // Pippenger MSM scratch per batch slot (msm.hpp: counts, offsets, level prefixes, sorted
+  // entries, bucket trees, bit-plane sums) and the slot's RLC seed (the bisection's k_vm_rs)
+  uint32_t* msm_buf[OVH_BATCH_SLOTS] = {};
+  uint64_t slot_seed[OVH_BATCH_SLOTS] = {}, slot_base[OVH_BATCH_SLOTS] = {};
   // Fp-VM programs + constant table in device memory
-  VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{};
+  VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{};
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
@@ -841,7 +883,7 @@ struct ovh_ctx {
     if (e_) return e_;              \
   } while (0)
 
-static const char* const STAGE_NAMES[OVH_NSTAGES] = {"hash_to_field", "vote", "fold", "final", "bisect"};
+static const char* const STAGE_NAMES[OVH_NSTAGES] = {"hash_to_field", "vote", "fold", "final", "bisect", "msm"};
 
 // LDS bytes of the VM kernels: constants + slices x slots (+ a 16-byte slice header for vote)
 static constexpr size_t LDS_VOTE = ((size_t)SLOT_BASE_W + VM_SLICES * (size_t)VOTE_STRIDE_W) * 4;
@@ -851,6 +893,18 @@ static constexpr size_t LDS_FINAL = ((size_t)SLOT_BASE_W + (size_t)VM_FINAL_NSLO
 static_assert(VM_VOTE_W * VM_SLICES == 64 && VM_VOTE_T_W * VM_SLICES == 64 && VM_FOLD_W * VM_FOLD_UNITS == 64 &&
                   VM_FINAL_W == 64, "VM slice widths");
 static constexpr size_t LDS_FOLD1 = ((size_t)SLOT_BASE_W + (size_t)FOLD_STRIDE_W) * 4;
+// bisection r sigma and the MSM pair kernels (8-lane madd / padd, 16-lane hdbl<m>)
+static constexpr size_t LDS_RS = ((size_t)SLOT_BASE_W + (64 / VM_RS_W) * (size_t)RS_STRIDE_W) * 4;
+constexpr uint32_t cmax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+static constexpr uint32_t MSM8_STRIDE_W = align128w(cmax(VM_MADD_NSLOTS, VM_PADD_NSLOTS) * 12);
+static constexpr uint32_t HDBL_STRIDE_W =
+    align128w(cmax(cmax(cmax(VM_HDBL1_NSLOTS, VM_HDBL2_NSLOTS), cmax(VM_HDBL4_NSLOTS, VM_HDBL8_NSLOTS)), VM_HDBL16_NSLOTS) * 12);
+static constexpr size_t LDS_MSM8 = ((size_t)SLOT_BASE_W + (64 / VM_MADD_W) * (size_t)MSM8_STRIDE_W) * 4;
+static constexpr size_t LDS_HDBL = ((size_t)SLOT_BASE_W + (64 / VM_HDBL1_W) * (size_t)HDBL_STRIDE_W) * 4;
+static_assert(VM_MADD_W == VM_PADD_W && VM_HDBL1_W == VM_HDBL2_W && VM_HDBL1_W == VM_HDBL4_W && VM_HDBL1_W == VM_HDBL8_W &&
+                  VM_HDBL1_W == VM_HDBL16_W && VM_MADD_NIN == 10 && VM_PADD_NIN == 12 && VM_HDBL1_NIN == 12,
+              "MSM program shapes (tools/fpvm/progs.py)");
+static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024, "default LDS limit");
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
 // allocation granules assumed)
@@ -901,6 +955,20 @@ static int vm_init(ovh_ctx* c) {
                 VM_FOLD_NOUT));
   CHK(vm_upload(c, c->vm_final, VM_FINAL_CODE, VM_FINAL_NPHASES, VM_FINAL_W, VM_FINAL_NW, VM_FINAL_IN, VM_FINAL_NIN, VM_FINAL_OUT,
                 VM_FINAL_NOUT));
+  CHK(vm_upload(c, c->vm_rs, VM_RS_CODE, VM_RS_NPHASES, VM_RS_W, VM_RS_NW, VM_RS_IN, VM_RS_NIN, VM_RS_OUT, 0));
+  CHK(vm_upload(c, c->vm_madd, VM_MADD_CODE, VM_MADD_NPHASES, VM_MADD_W, VM_MADD_NW, VM_MADD_IN, VM_MADD_NIN, VM_MADD_OUT,
+                VM_MADD_NOUT));
+  CHK(vm_upload(c, c->vm_padd, VM_PADD_CODE, VM_PADD_NPHASES, VM_PADD_W, VM_PADD_NW, VM_PADD_IN, VM_PADD_NIN, VM_PADD_OUT,
+                VM_PADD_NOUT));
+#define UPLOAD_HDBL(k, M)                                                                                               \
+  CHK(vm_upload(c, c->vm_hdbl[k], VM_HDBL##M##_CODE, VM_HDBL##M##_NPHASES, VM_HDBL##M##_W, VM_HDBL##M##_NW, VM_HDBL##M##_IN, \
+                VM_HDBL##M##_NIN, VM_HDBL##M##_OUT, VM_HDBL##M##_NOUT))
+  UPLOAD_HDBL(0, 1);
+  UPLOAD_HDBL(1, 2);
+  UPLOAD_HDBL(2, 4);
+  UPLOAD_HDBL(3, 8);
+  UPLOAD_HDBL(4, 16);
+#undef UPLOAD_HDBL
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote_t, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE_T));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold<VM_FOLD_UNITS>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -948,8 +1016,41 @@ static int sync_all(ovh_ctx* c) {
   return 0;
 }
 
-// Batch state for n votes: per slot S_TOTAL planes, fold regions R0..R3 (cap/4 partials each)
-// and the group verdicts. A reallocation waits for all work and forgets the last batch.
+// MSM scratch of a slot (msm.hpp MsmArgs), in words: cnt, off, cur, level prefixes, entries
+// (2 points x 4 windows per vote), bucket trees (level-0 outputs: <= 4 cap + NB), U planes.
+static size_t msm_acap(uint32_t cap) { return (size_t)4 * cap + MSM_NB; }
+static size_t msm_round(size_t w) { return (w + 63) / 64 * 64; }
+static size_t msm_words(uint32_t cap) {
+  return msm_round(MSM_NB) + msm_round(MSM_NB + 1) + msm_round(MSM_NB) + msm_round((size_t)MSM_LV * (MSM_NB + 1)) +
+         msm_round((size_t)8 * cap) + msm_round((size_t)6 * 12 * msm_acap(cap)) + (size_t)6 * 12 * MSM_U;
+}
+static MsmArgs msm_args(ovh_ctx* c, int slot, uint32_t** cur) {
+  uint32_t* p = c->msm_buf[slot];
+  MsmArgs a;
+  a.cnt = p;
+  p += msm_round(MSM_NB);
+  a.off = p;
+  p += msm_round(MSM_NB + 1);
+  *cur = p;
+  p += msm_round(MSM_NB);
+  a.pf = p;
+  p += msm_round((size_t)MSM_LV * (MSM_NB + 1));
+  a.ent = p;
+  p += msm_round((size_t)8 * c->cap);
+  a.A = Slab{p, (uint32_t)msm_acap(c->cap)};
+  p += msm_round((size_t)6 * 12 * msm_acap(c->cap));
+  a.U = Slab{p, MSM_U};
+  a.st = Slab{c->state_slot[slot], c->cap};
+  return a;
+}
+static Slab msm_S(ovh_ctx* c, int slot) {
+  uint32_t* cur;
+  return msm_args(c, slot, &cur).U;  // element 0: sum r_i sigma_i
+}
+
+// Batch state for n votes: per slot S_TOTAL planes, fold regions R0..R3 (cap/4 partials each),
+// the group verdicts and the MSM scratch. A reallocation waits for all work and forgets the
+// last batch.
 static int ensure_cap(ovh_ctx* c, size_t n) {
   if (n > (1u << 24)) return OVH_ERR_ARG;
   if (n <= c->cap && c->state_slot[0]) return 0;
@@ -957,9 +1058,9 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
   while (cap < n) cap <<= 1;
   CHK(sync_all(c));
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
-    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k]})
+    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k]})
       if (p) (void)hipFree(p);
-    c->state_slot[k] = c->red_slot[k] = nullptr;
+    c->state_slot[k] = c->red_slot[k] = c->msm_buf[k] = nullptr;
     c->grp_ok[k] = nullptr;
     c->slot_n[k] = 0;
   }
@@ -970,6 +1071,7 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
     HIPCHK(hipMalloc(&c->state_slot[k], (size_t)S_TOTAL * 12 * cap * 4));
     HIPCHK(hipMalloc(&c->red_slot[k], (size_t)4 * PART_PLANES * 12 * c->red_cap * 4));
     HIPCHK(hipMalloc(&c->grp_ok[k], ((size_t)cap / GROUP_VOTES + 1) * 4));
+    HIPCHK(hipMalloc(&c->msm_buf[k], msm_words(cap) * 4));
   }
   c->cap = cap;
   return 0;
@@ -1057,6 +1159,8 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   c->ev_mask = 0;
   uint64_t seed, base;
   CHK(draw_seed(c, &seed, &base));
+  c->slot_seed[slot] = seed;
+  c->slot_base[slot] = base;
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
   if (pipelined) {  // hash_to_field on hstream once the previous vote kernel finished: it runs
                     // beside that batch's fold levels (a few workgroups) instead of before this
@@ -1122,10 +1226,48 @@ static int fold_down(ovh_ctx* c, int slot, hipStream_t st, int slices, int* reg,
 enum { RES_BATCH = 4, RES_COMBINE = RES_BATCH + OVH_BATCH_SLOTS, RES_SYNC = RES_COMBINE + OVH_BATCH_SLOTS, RES_MULTI };
 static_assert(RES_MULTI < 16, "verdict words fit c->result");
 
-// Final check on <= 4 partials given as planes: k_vm_final on stream `st`, verdict to *d_res.
-static void enqueue_final(ovh_ctx* c, hipStream_t st, Slab F, Slab S, uint32_t m, int32_t* d_res) {
+// Final check on <= 4 partials given as planes: k_vm_final on stream `st`, verdict to *d_res;
+// xS: the batch's MSM result (partial 0's S), or {nullptr} when the partials carry their S.
+static void enqueue_final(ovh_ctx* c, hipStream_t st, Slab F, Slab S, uint32_t m, int32_t* d_res,
+                          Slab xS = Slab{nullptr, 0}) {
   StageScope p(c, ST_FINAL, st);
-  k_vm_final<<<1, 64, LDS_FINAL, st>>>(m, c->vm_final, c->vm_consts, F, S, d_res);
+  k_vm_final<<<1, 64, LDS_FINAL, st>>>(m, c->vm_final, c->vm_consts, F, S, xS, d_res);
+}
+
+// Pippenger MSM of the batch in `slot` on stream st (msm.hpp): S = sum of r_i sigma_i over the
+// votes with code 0 -> msm_S(c, slot). Needs the vote kernel's codes and sigma / tau planes.
+static int enqueue_msm(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, const int32_t* d_codes) {
+  StageScope p(c, ST_MSM, st);
+  uint32_t* cur;
+  const MsmArgs a = msm_args(c, slot, &cur);
+  const uint64_t seed = c->slot_seed[slot], base = c->slot_base[slot];
+  uint32_t nlev = 1;  // tree levels: 2^nlev >= the largest possible bucket (2n points)
+  while ((1ull << nlev) < 2ull * n) ++nlev;
+  if (nlev > MSM_LV) return OVH_ERR_ARG;
+  HIPCHK(hipMemsetAsync((void*)a.cnt, 0, MSM_NB * 4, st));
+  const uint32_t nb = (n + 255) / 256;
+  k_msm_count<<<nb, 256, 0, st>>>(n, seed, base, d_codes, (uint32_t*)a.cnt);
+  k_msm_scan<<<1, 1024, 0, st>>>(nlev, a.cnt, (uint32_t*)a.off, cur, (uint32_t*)a.pf);
+  k_msm_scatter<<<nb, 256, 0, st>>>(n, seed, base, d_codes, cur, (uint32_t*)a.ent);
+  constexpr uint32_t SL8 = 64 / VM_MADD_W, SL16 = 64 / VM_HDBL1_W;
+  auto grid = [](uint64_t pairs, uint32_t sl) { return (uint32_t)((pairs + sl - 1) / sl); };
+  // bucket trees: level 0 pairs (<= 4n + NB), level l (<= 8n / 2^(l+1) + NB), in place
+  k_msm_pair<VM_MADD_W, MSM_L0><<<grid(4ull * n + MSM_NB, SL8), 64, LDS_MSM8, st>>>(0, c->vm_madd, VM_MADD_NIN,
+                                                                                     MSM8_STRIDE_W, c->vm_consts, a);
+  for (uint32_t lv = 1; lv < nlev; ++lv)
+    k_msm_pair<VM_PADD_W, MSM_LVL><<<grid((8ull * n >> (lv + 1)) + MSM_NB, SL8), 64, LDS_MSM8, st>>>(
+        lv, c->vm_padd, VM_PADD_NIN, MSM8_STRIDE_W, c->vm_consts, a);
+  // bit-plane sums T_t (128 buckets each): pairs of buckets, then 6 levels
+  k_msm_pair<VM_PADD_W, MSM_T0><<<grid(MSM_U, SL8), 64, LDS_MSM8, st>>>(0, c->vm_padd, VM_PADD_NIN, MSM8_STRIDE_W,
+                                                                        c->vm_consts, a);
+  for (uint32_t lv = 1; lv <= 6; ++lv)
+    k_msm_pair<VM_PADD_W, MSM_TL><<<grid(MSM_NT * (MSM_TM >> lv), SL8), 64, LDS_MSM8, st>>>(
+        lv, c->vm_padd, VM_PADD_NIN, MSM8_STRIDE_W, c->vm_consts, a);
+  // sum_t 2^t T_t: five levels of A + [2^m] B, m = 1, 2, 4, 8, 16
+  for (uint32_t h = 1; h <= 5; ++h)
+    k_msm_pair<VM_HDBL1_W, MSM_HRN><<<grid(MSM_NT >> h, SL16), 64, LDS_HDBL, st>>>(
+        h, c->vm_hdbl[h - 1], VM_HDBL1_NIN, HDBL_STRIDE_W, c->vm_consts, a);
+  return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
 }
 
 // Bisection of the batch in `slot` on stream `st`, skipped on the device when *d_verdict == 1
@@ -1135,6 +1277,17 @@ static void enqueue_bisect(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, int
                            const int32_t* d_verdict) {
   StageScope p(c, ST_FALLBACK, st);
   const uint32_t g = groups_of(n);
+  // r_i sigma_i per vote, then fold levels 0 and 1 of (f, r sigma) -> R1 (16-vote groups)
+  Slab s{c->state_slot[slot], c->cap};
+  k_vm_rs<<<(n + 64 / VM_RS_W - 1) / (64 / VM_RS_W), 64, LDS_RS, st>>>(n, c->vm_rs, c->vm_consts, s, c->slot_seed[slot],
+                                                                     c->slot_base[slot], d_codes, d_verdict);
+  const uint32_t nwg = (n + 3) / 4;
+  k_vm_fold<VM_FOLD_UNITS><<<(nwg + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(
+      n, c->vm_fold, c->vm_consts, Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{s.p + (size_t)S_RS * 12 * s.cap, s.cap},
+      region_F(c, slot, 0), d_codes, d_verdict);
+  k_vm_fold<VM_FOLD_UNITS><<<(g + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(
+      nwg, c->vm_fold, c->vm_consts, region_F(c, slot, 0), region_S(c, slot, 0), region_F(c, slot, 1), nullptr,
+      d_verdict);
   k_vm_group<<<g, 64, LDS_FINAL, st>>>(g, c->vm_final, c->vm_consts, region_F(c, slot, 1), region_S(c, slot, 1),
                                        d_verdict, c->grp_ok[slot]);
   k_vm_votechk<<<n, 64, LDS_FINAL, st>>>(n, c->vm_final, c->vm_consts, Slab{c->state_slot[slot], c->cap}, d_codes,
@@ -1158,7 +1311,8 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
   hipStream_t fst = c->fs[slot];
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
   int32_t* verdict = c->result + RES_BATCH + slot;
-  enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict);
+  CHK(enqueue_msm(c, fst, slot, (uint32_t)n, d_codes));
+  enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict, msm_S(c, slot));
   enqueue_bisect(c, fst, slot, (uint32_t)n, d_codes, verdict);
   HIPCHK(hipEventRecord(c->ev_back[slot], fst));
   HIPCHK(hipGetLastError());
@@ -1211,16 +1365,18 @@ static int verify_host_locked(ovh_ctx* c, size_t n, const uint8_t* sigs, const u
   return 0;
 }
 
-// Per-shard partial of `slot` (folded to one) -> AoS at `out` (device), on the main stream.
-static int shard_partial(ovh_ctx* c, int slot, uint32_t n, uint32_t* out, hipStream_t wait_on) {
+// Per-shard partial of `slot` (f folded to one, S from the MSM) -> AoS at `out` (device), on
+// the main stream.
+static int shard_partial(ovh_ctx* c, int slot, uint32_t n, const int32_t* d_codes, uint32_t* out, hipStream_t wait_on) {
   uint32_t m = groups_of(n);
   int reg = 1;
   CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 1));
+  CHK(enqueue_msm(c, c->stream, slot, n, d_codes));
   if (wait_on) {  // the caller's earlier work on its stream (e.g. a gather reading `out`) first
     HIPCHK(hipEventRecord(c->ev_x[0], wait_on));
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_x[0], 0));
   }
-  k_pack_partial2<<<1, 64, 0, c->stream>>>(region_F(c, slot, reg), region_S(c, slot, reg), out);
+  k_pack_partial2<<<1, 64, 0, c->stream>>>(region_F(c, slot, reg), msm_S(c, slot), out);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1262,7 +1418,7 @@ static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
     CHK(take_slot(s, &slot[d]));
     s->test_base = root->test_base + lo;  // OVH_FLAG_TEST_RLC only: one global index per vote
     CHK(batch_front(s, slot[d], (uint32_t)cnt, in, in + cnt * 96, key, dcodes[d], false));
-    CHK(shard_partial(s, slot[d], (uint32_t)cnt, s->part_out, nullptr));
+    CHK(shard_partial(s, slot[d], (uint32_t)cnt, dcodes[d], s->part_out, nullptr));
     // partial -> devices[0] (peer copy over xGMI), ordered on this device's stream
     HIPCHK(hipMemcpyPeerAsync(root->gather + k * OVH_PARTIAL_BYTES, s0->device, s->part_out, s->device,
                               OVH_PARTIAL_BYTES, s->stream));
@@ -1442,7 +1598,7 @@ static void destroy_one(ovh_ctx* c) {
   for (hipStream_t s : {c->fstream, c->fstream2})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
-    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k]})
+    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k]})
       if (p) (void)hipFree(p);
   for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vm_consts,
                   (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
@@ -1584,7 +1740,8 @@ int ovh_verify(ovh_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* ha
     int slot;
     CHK(take_slot(s, &slot));
     CHK(batch_front(s, slot, 1, d, d + 96, key, dc, false));
-    enqueue_final(s, s->stream, region_F(s, slot, 1), region_S(s, slot, 1), 1, s->result);
+    CHK(enqueue_msm(s, s->stream, slot, 1, dc));
+    enqueue_final(s, s->stream, region_F(s, slot, 1), region_S(s, slot, 1), 1, s->result, msm_S(s, slot));
     HIPCHK(hipGetLastError());
     int32_t out[2] = {-1, -1};
     HIPCHK(hipMemcpyAsync(&out[0], dc, 4, hipMemcpyDeviceToHost, s->stream));
@@ -2079,7 +2236,7 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   int slot;
   CHK(take_slot(c, &slot));
   CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false));
-  CHK(shard_partial(c, slot, (uint32_t)n, (uint32_t*)d_partial, st));
+  CHK(shard_partial(c, slot, (uint32_t)n, d_codes, (uint32_t*)d_partial, st));
   if (st) {
     HIPCHK(hipEventRecord(c->ev_x[1], c->stream));
     HIPCHK(hipStreamWaitEvent(st, c->ev_x[1], 0));

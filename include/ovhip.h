@@ -52,7 +52,7 @@ typedef struct ovh_ctx ovh_ctx;
                                            SecretKey::from_bytes) instead of KeyGen (see ovh_sk_parse) */
 
 /* Batch stages (ovh_stage_name gives the label). Each stage is one or more kernels. */
-#define OVH_NSTAGES 5
+#define OVH_NSTAGES 6
 
 /* Create a context on HIP device `device` with hash-to-curve domain separation tag `dst`
  * (NULL -> "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_", the believed ophelia-blst DST).

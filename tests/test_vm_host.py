@@ -101,7 +101,7 @@ def test_vote_program_on_interpreter(hx, built, golden_votes, any_all):  # noqa:
 @pytest.mark.parametrize("any_all", [0, 1])
 def test_vote_t_program_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
     """vote_t (key from the validator table, projective) on the golden votes: interpreter ==
-    simulator, and the same r sigma as the vote program."""
+    simulator, and the same sigma / tau (the MSM's points) as the vote program."""
     consts, progs_ = built
     _, vsc, vwords, _, _ = progs_["vote"]
     prog, sc, words, _, _ = progs_["vote_t"]
@@ -116,18 +116,25 @@ def test_vote_t_program_on_interpreter(hx, built, golden_votes, any_all):  # noq
         sim = sched.simulate(sc, words, tin, r)
         assert_same(run_vm(hx, consts, sc, words, tin, r, any_all), sim, "vote_t %d" % k)
         vsim = sched.simulate(vsc, vwords, inp, r)
-        assert [sim["st:s%d" % j] for j in range(6)] == [vsim["st:s%d" % j] for j in range(6)]
+        qt = ["st:q%d" % j for j in range(4)] + ["st:t%d" % j for j in range(4)]
+        assert [sim[n] for n in qt] == [vsim[n] for n in qt]
 
 
 @pytest.mark.parametrize("any_all", [0, 1])
 def test_fold_final_bisect_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
     consts, progs_ = built
     prog, sc, words, _, _ = progs_["vote"]
+    _, rsc, rwords, _, _ = progs_["rs"]
     r = 0x1234567890ABCDEF
     parts = []
     for inp in golden_votes[:2]:
         o = sched.simulate(sc, words, inp, r)
         o = {(n[3:] if n.startswith("st:") else n): v for n, v in o.items()}
+        # the bisection's r sigma from the stored sigma / tau (program rs), interpreter == simulator
+        rin = {n: o[n] for n in progs.RS_IN}
+        rsim = sched.simulate(rsc, rwords, rin, r)
+        assert_same(run_vm(hx, consts, rsc, rwords, rin, r, any_all), rsim, "rs")
+        o.update({n[3:]: v for n, v in rsim.items()})
         parts.append(o)
 
     def final_in(items):
@@ -152,6 +159,28 @@ def test_fold_final_bisect_on_interpreter(hx, built, golden_votes, any_all):  # 
         sim = sched.simulate(psc, pwords, pin)
         assert sim == {"ok": want}
         assert_same(run_vm(hx, consts, psc, pwords, pin, 0, any_all), sim, "final/bisect")
+
+
+@pytest.mark.parametrize("any_all", [0, 1])
+def test_msm_programs_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
+    """The MSM pair programs (madd, padd, hdbl<m>) through the interpreter == simulator on golden
+    signature points, identity operands and the doubling case (gen.check_msm ties the programs'
+    values to the oracle's point arithmetic)."""
+    consts, progs_ = built
+    bls = gen._oracle()
+    with open(os.path.join(ROOT, "tests", "golden", "golden_v1.json")) as fh:
+        g = json.load(fh)
+    A, B = (bls.g2_from_bytes(bytes.fromhex(v["sig"])) for v in g["votes"][:2])
+    for name, (prog, sc, words, ins, outs) in progs_.items():
+        if name not in ("madd", "padd") and not name.startswith("hdbl"):
+            continue
+        for X, Y in ((A, B), (A, A), (B, None), (None, B)):
+            if name == "madd" and X is None:
+                continue
+            xa = [X[0][0], X[0][1], X[1][0], X[1][1]] if name == "madd" else gen._proj(X, (7, 2))
+            inp = dict(zip(ins, xa + gen._proj(Y)))
+            sim = sched.simulate(sc, words, inp)
+            assert_same(run_vm(hx, consts, sc, words, inp, 0, any_all), sim, name)
 
 
 def test_fp_inv(hx):

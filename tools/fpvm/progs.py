@@ -3,9 +3,15 @@ layouts. Input and output names are listed in the order the HIP side addresses t
 
   vote     one vote of ovh_verify_batch: pk decompress + G1 subgroup
            check, sig decompress + G2 subgroup check, hash_to_G2 from (u0, u1), the RLC
-           scalar products r pk and r sigma (projective), f = Miller(r pk, H).
+           scalar product r pk (projective), f = Miller(r pk, H); stores f, sigma and
+           tau = -psi^2(sigma) (affine) for the Pippenger MSM of sum r_i sigma_i
   vote_t   the same for a public key taken from the device validator table (ovh_set_validators:
            already decompressed and group-checked, projective) or a QC's aggregated key.
+  rs       bisection only: r sigma = [a] sigma + [b] tau for one vote (the per-vote term the MSM
+           sums), 32-step joint chain
+  madd     MSM bucket level 0: B (projective) + A (affine)
+  padd     MSM bucket levels >= 1 and the bit-plane sums: A + B (projective)
+  hdbl<m>  MSM window combination: A + [2^m] B (projective), m = 1, 2, 4, 8, 16
   fold     4 partials (F_i in Fp12, S_i projective G2) -> (prod F_i, sum S_i)
   final    up to 4 partials -> prod F * Miller(-G1, sum S) -> final exponentiation == 1; also
            the bisection checks of the fallback (one group's partial, or one vote's (f, r sigma):
@@ -46,14 +52,21 @@ def unflat_g2p(v):
     return (tuple(v[0:2]), tuple(v[2:4]), tuple(v[4:6]))
 
 
-# HBM state planes of a vote (ovhip.hip reads them through VM_S_* in vm_progs.inc)
-S_U, S_RS, S_F, S_TOTAL = 0, 4, 10, 22
+# HBM state planes of a vote (ovhip.hip reads them through VM_S_* in vm_progs.inc):
+# u0, u1 | sigma affine | tau = -psi^2(sigma) affine | f | r sigma (bisection only)
+S_U, S_SIG, S_TAU, S_F, S_RS, S_TOTAL = 0, 4, 8, 12, 24, 30
 
 VOTE_IN = ["pk_x", "pk_sort", "sig_x0", "sig_x1", "sig_sort", "u00", "u01", "u10", "u11"]
 VOTE_OUT = ["pk_ok", "pk_grp", "sig_ok", "sig_grp", "h_inf"]
 # stored straight to HBM planes by `st` ops as soon as they are final
 VOTE_ST = [(n, S_F + k) for k, n in enumerate(f12_names("f"))] + \
-    [(n, S_RS + k) for k, n in enumerate(g2p_names("s"))]
+    [("q%d" % k, S_SIG + k) for k in range(4)] + [("t%d" % k, S_TAU + k) for k in range(4)]
+
+
+def affine_pair(a, Q):
+    """sigma (affine) and tau = -psi^2(sigma) (affine: psi^2 keeps Z = 1) as 8 Fp values."""
+    T = a.g2_neg_psi2(Q)
+    return [Q[0][0], Q[0][1], Q[1][0], Q[1][1], T[0][0], T[0][1], T[1][0], T[1][1]]
 
 
 def build_vote():
@@ -73,11 +86,10 @@ def build_vote():
     H = a.hash_to_g2(u0, u1)
     h_inf = a.f2_is_zero(H[2])
     rP = a.pt_mul_glv("fp", Pp, a.g1_phi(Pp))          # projective: no inversion
-    rS = a.pt_mul_glv("f2", Qs, a.g2_neg_psi2(Qs))
     f = a.miller_loop(rP, H)
     for name, v in zip(VOTE_OUT, [pk_ok, pk_grp, sig_ok, sig_grp, h_inf]):
         p.output(name, v)
-    for (name, plane), v in zip(VOTE_ST, flat12(f) + flat_g2p(rS)):
+    for (name, plane), v in zip(VOTE_ST, flat12(f) + affine_pair(a, Qs)):
         p.store(name, v, plane)
     return p
 
@@ -100,13 +112,82 @@ def build_vote_t():
     H = a.hash_to_g2(u0, u1)
     h_inf = a.f2_is_zero(H[2])
     rP = a.pt_mul_glv("fp", Pp, a.g1_phi(Pp))
-    rS = a.pt_mul_glv("f2", Qs, a.g2_neg_psi2(Qs))
     f = a.miller_loop(rP, H)
     for name, v in zip(VOTE_T_OUT, [sig_ok, sig_grp, h_inf]):
         p.output(name, v)
-    for (name, plane), v in zip(VOTE_ST, flat12(f) + flat_g2p(rS)):
+    for (name, plane), v in zip(VOTE_ST, flat12(f) + affine_pair(a, Qs)):
         p.store(name, v, plane)
     return p
+
+
+RS_IN = ["q%d" % k for k in range(4)] + ["t%d" % k for k in range(4)]
+RS_OUT = []
+RS_ST = [(n, S_RS + k) for k, n in enumerate(g2p_names("s"))]
+
+
+def build_rs():
+    """[a] sigma + [b] tau for the vote's RLC value (a, b its 32-bit halves): the vote's r sigma,
+    recomputed by the bisection when the batch's combined check failed."""
+    p = Prog("rs")
+    a = Alg(p, use_sop=USE_SOP)
+    one = (p.one, p.zero)
+    Q = ((p.input("q0"), p.input("q1")), (p.input("q2"), p.input("q3")), one)
+    T = ((p.input("t0"), p.input("t1")), (p.input("t2"), p.input("t3")), one)
+    rS = a.pt_mul_glv("f2", Q, T)
+    for (name, plane), v in zip(RS_ST, flat_g2p(rS)):
+        p.store(name, v, plane)
+    return p
+
+
+# ---- Pippenger MSM of sum r_i sigma_i (ovhip.hip k_msm_*): points are projective (X : Y : Z)
+AFF_IN = ["a%d" % k for k in range(4)]
+PA_IN = ["a%d" % k for k in range(6)]
+PB_IN = ["b%d" % k for k in range(6)]
+PT_OUT = ["s%d" % k for k in range(6)]
+
+
+def _pt_in(p, names):
+    v = [p.input(n) for n in names]
+    return unflat_g2p(v) if len(v) == 6 else ((v[0], v[1]), (v[2], v[3]), (p.one, p.zero))
+
+
+def build_madd():
+    """bucket level 0: B + A, A affine (a point of the sorted entry list), B projective (the
+    pair's other point with Z = 1, or the identity (0 : 1 : 0) for a bucket's odd last entry)."""
+    p = Prog("madd")
+    a = Alg(p, use_sop=USE_SOP)
+    A = _pt_in(p, AFF_IN)
+    B = _pt_in(p, PB_IN)
+    for name, v in zip(PT_OUT, flat_g2p(a.pt_add("f2", B, A))):
+        p.output(name, v)
+    return p
+
+
+def build_padd():
+    p = Prog("padd")
+    a = Alg(p, use_sop=USE_SOP)
+    S = a.pt_add("f2", _pt_in(p, PA_IN), _pt_in(p, PB_IN))
+    for name, v in zip(PT_OUT, flat_g2p(S)):
+        p.output(name, v)
+    return p
+
+
+HDBL_M = (1, 2, 4, 8, 16)
+
+
+def build_hdbl(m):
+    """A + [2^m] B: one level of the MSM's window combination sum_t 2^t T_t (pairs of levels
+    2^(2^(h-1)) apart)."""
+    def build():
+        p = Prog("hdbl%d" % m)
+        a = Alg(p, use_sop=USE_SOP)
+        B = _pt_in(p, PB_IN)
+        for _ in range(m):
+            B = a.pt_dbl("f2", B)
+        for name, v in zip(PT_OUT, flat_g2p(a.pt_add("f2", _pt_in(p, PA_IN), B))):
+            p.output(name, v)
+        return p
+    return build
 
 
 FOLD_K = 4
@@ -160,4 +241,9 @@ PROGRAMS = {
     "vote_t": (build_vote_t, VOTE_T_IN, VOTE_T_OUT),
     "fold": (build_fold, FOLD_IN, FOLD_OUT),
     "final": (build_final, FINAL_IN, FINAL_OUT),
+    "rs": (build_rs, RS_IN, RS_OUT),
+    "madd": (build_madd, AFF_IN + PB_IN, PT_OUT),
+    "padd": (build_padd, PA_IN + PB_IN, PT_OUT),
 }
+for _m in HDBL_M:
+    PROGRAMS["hdbl%d" % _m] = (build_hdbl(_m), PA_IN + PB_IN, PT_OUT)
