@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
+#include <stdlib.h>
 #include <sys/random.h>
 #include <sys/types.h>
 
@@ -268,8 +269,9 @@ __device__ __forceinline__ void vote_stagger() {
 __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
                                                 const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
                                                 Slab s, uint64_t seed, uint64_t base, int32_t* __restrict__ codes,
-                                                Slab part0) {
+                                                Slab part0, unsigned long long* vstart) {
   __builtin_amdgcn_s_setprio(2);  // per-vote stages outrank a co-resident final-stream wave
+  if (vstart && threadIdx.x == 0) atomicAdd(vstart, 1ull);  // resident (k_gate)
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -412,8 +414,10 @@ struct PkSrc {
 // (code, stored f and r sigma, fused level-0 fold) as k_vm_vote.
 __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
                                                   PkSrc pk, const uint8_t* __restrict__ sigs, Slab s, uint64_t seed,
-                                                  uint64_t base, int32_t* __restrict__ codes, Slab part0) {
+                                                  uint64_t base, int32_t* __restrict__ codes, Slab part0,
+                                                  unsigned long long* vstart) {
   __builtin_amdgcn_s_setprio(2);
+  if (vstart && threadIdx.x == 0) atomicAdd(vstart, 1ull);
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -553,6 +557,19 @@ __global__ __launch_bounds__(64) void k_vm_rs(uint32_t n, VmDev prog, const uint
 }
 
 #include "msm.hpp"
+
+#define GATE_TICKS 30000ull  // 300 us of the 100 MHz wall clock
+// Pipelined batches: holds a final stream until the next vote kernel's workgroups are resident
+// (the vote kernels count their started workgroups into *vstart; target = that count once the
+// next kernel's are placed), so no final-stream workgroup takes the LDS a vote workgroup needs
+// (a vote workgroup that finds none waits for a whole vote duration); gives up after `ticks` of
+// the 100 MHz wall clock (no next batch in flight).
+__global__ __launch_bounds__(64) void k_gate(const unsigned long long* vstart, unsigned long long target, uint64_t ticks) {
+  if (threadIdx.x) return;
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(vstart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && wall_clock64() - t0 < ticks)
+    __builtin_amdgcn_s_sleep(16);
+}
 
 // Validator table (ovh_set_validators): lane per key, 48-byte compressed -> flags + the point
 // (X : Y : Z) Montgomery, (0 : 1 : 0) for infinity or a failed parse.
@@ -821,11 +838,8 @@ struct ovh_ctx {
   // SIMD with a vote wave and takes longer than a vote kernel there).
   hipStream_t fstream = nullptr, fstream2 = nullptr;
   hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
-  hipStream_t hstream = nullptr;  // hash_to_field of the next batch, beside the current vote
-  hipEvent_t ev_h[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
-  hipEvent_t ev_vote = nullptr;  // after the latest pipelined vote kernel (batch_front)
   uint32_t* state_slot[OVH_BATCH_SLOTS] = {};
   uint32_t* red_slot[OVH_BATCH_SLOTS] = {};  // fold regions R0..R3 (R1: the 16-vote groups)
   int32_t* grp_ok[OVH_BATCH_SLOTS] = {};
@@ -833,6 +847,9 @@ struct ovh_ctx {
   uint32_t* fin = nullptr;  // OVH_BATCH_SLOTS x FIN_STRIDE words: per-slot combine scratch
   uint32_t pipe_k = 0;
   int last_slot = 0;
+  // pipeline placement (environment OVH_FOLD_SIDE, read at ovh_create): 1 (default) runs the
+  // fold levels on the final stream instead of between two vote kernels on the main stream
+  bool fold_side = true;
   XmdTemplates xmd;
   std::mutex mu;  // Crypto is Send + Sync: every entry point holds it for its whole call
   uint32_t cap = 0, red_cap = 0;
@@ -846,6 +863,9 @@ struct ovh_ctx {
   uint32_t comb_cap = 0;
   uint32_t* part_out = nullptr;  // multi-device: this device's partial (216 words)
   int32_t* result = nullptr;     // device verdict words
+  unsigned long long* vstart = nullptr;  // vote workgroups started (k_gate), device
+  uint64_t vlaunched = 0;                // vote workgroups launched, host
+  uint32_t wg_cap = 1024;                // vote workgroups resident at once (4 per CU)
   uint32_t last_n = 0;
   // RLC coefficients: fresh getrandom seed per batch, or the test seed (OVH_FLAG_TEST_RLC)
   uint64_t test_seed = 0, test_base = 0;
@@ -1012,7 +1032,6 @@ static int sync_all(ovh_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->fstream));
   HIPCHK(hipStreamSynchronize(c->fstream2));
-  HIPCHK(hipStreamSynchronize(c->hstream));
   return 0;
 }
 
@@ -1153,7 +1172,7 @@ struct KeySrc {
 // Per-vote stages of a batch in `slot`: hash_to_field, the vote kernel with fold level 0 fused
 // (-> R0), fold level 1 (-> R1: one partial per 16-vote group, kept for the bisection).
 static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
-                       int32_t* d_codes, bool pipelined) {
+                       int32_t* d_codes, bool fold1 = true) {
   Slab s{c->state_slot[slot], c->cap};
   hipStream_t st = c->stream;
   c->ev_mask = 0;
@@ -1162,17 +1181,8 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   c->slot_seed[slot] = seed;
   c->slot_base[slot] = base;
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
-  if (pipelined) {  // hash_to_field on hstream once the previous vote kernel finished: it runs
-                    // beside that batch's fold levels (a few workgroups) instead of before this
-                    // vote on the main stream, and never beside a vote kernel
-    HIPCHK(hipStreamWaitEvent(c->hstream, c->ev_vote, 0));
-    {
-      StageScope p(c, ST_H2F, c->hstream);
-      k_h2f<<<nblk(n), WG, 0, c->hstream>>>(n, d_hashes, c->xmd, s);
-    }
-    HIPCHK(hipEventRecord(c->ev_h[slot], c->hstream));
-    HIPCHK(hipStreamWaitEvent(st, c->ev_h[slot], 0));
-  } else {
+  {  // hash_to_field on the main stream: its inputs are ready in that stream's order (the
+     // staging copies, or a caller's writes on ovh_stream)
     StageScope p(c, ST_H2F);
     k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s);
   }
@@ -1180,13 +1190,13 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
     StageScope p(c, ST_VOTE);
     if (key.bytes)
       k_vm_vote<<<nwg, 64, LDS_VOTE, st>>>(n, c->vm_vote, c->vm_fold, c->vm_consts, key.bytes, d_sigs, s, seed, base,
-                                           d_codes, region_F(c, slot, 0));
+                                           d_codes, region_F(c, slot, 0), c->vstart);
     else
       k_vm_vote_t<<<nwg, 64, LDS_VOTE_T, st>>>(n, c->vm_vote_t, c->vm_fold, c->vm_consts, key.pts, d_sigs, s, seed,
-                                               base, d_codes, region_F(c, slot, 0));
+                                               base, d_codes, region_F(c, slot, 0), c->vstart);
+    c->vlaunched += nwg;
   }
-  if (pipelined) HIPCHK(hipEventRecord(c->ev_vote, st));
-  {  // fold level 1: R0 -> R1 (one partial per 16-vote group, kept for the bisection)
+  if (fold1) {  // fold level 1: R0 -> R1 (one partial per 16-vote group)
     StageScope p(c, ST_FOLD);
     const uint32_t m1 = (nwg + 3) / 4;
     k_vm_fold<VM_FOLD_UNITS><<<(m1 + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(
@@ -1296,20 +1306,34 @@ static void enqueue_bisect(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, int
 
 // One batch, pipelined: per-vote stages + wide fold levels on the main stream; the narrow fold
 // levels, the combined check and the gated bisection on the final stream. Caller holds c->mu.
+// pipe (ovh_verify_batch_device_async): the final stream first waits (k_gate) until the next
+// batch's vote workgroups are resident.
 static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
-                               int32_t* d_codes) {
+                               int32_t* d_codes, bool pipe = false) {
   CHK(ensure_cap(c, n));
   int slot;
   CHK(take_slot(c, &slot));
-  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, true));
+  const bool side = c->fold_side;
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, !side));
+  hipStream_t fst = c->fs[slot];
   uint32_t m = groups_of((uint32_t)n);
   int reg = 1;
-  // every fold level on the main stream (it idles while a final runs): the final streams carry
-  // only the finals and the bisections, and no fold workgroup competes with a vote for LDS
-  CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 4));
-  HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
-  hipStream_t fst = c->fs[slot];
-  HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
+  const uint32_t nwg = ((uint32_t)n + VM_SLICES - 1) / VM_SLICES;
+  if (side) {  // fold levels on the final stream, beside the next batch's vote kernel
+    HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
+    HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
+    if (pipe) k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
+    k_vm_fold<VM_FOLD_UNITS><<<(m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, fst>>>(
+        nwg, c->vm_fold, c->vm_consts, region_F(c, slot, 0), region_S(c, slot, 0), region_F(c, slot, 1), nullptr);
+    CHK(fold_down(c, slot, fst, VM_SLICES, &reg, &m, 4));
+  } else {
+    // every fold level on the main stream (it idles while a final runs): the final streams carry
+    // only the MSM, the finals and the bisections
+    CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 4));
+    HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
+    HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
+    if (pipe) k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
+  }
   int32_t* verdict = c->result + RES_BATCH + slot;
   CHK(enqueue_msm(c, fst, slot, (uint32_t)n, d_codes));
   enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict, msm_S(c, slot));
@@ -1417,7 +1441,7 @@ static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
     CHK(ensure_cap(s, cnt));
     CHK(take_slot(s, &slot[d]));
     s->test_base = root->test_base + lo;  // OVH_FLAG_TEST_RLC only: one global index per vote
-    CHK(batch_front(s, slot[d], (uint32_t)cnt, in, in + cnt * 96, key, dcodes[d], false));
+    CHK(batch_front(s, slot[d], (uint32_t)cnt, in, in + cnt * 96, key, dcodes[d]));
     CHK(shard_partial(s, slot[d], (uint32_t)cnt, dcodes[d], s->part_out, nullptr));
     // partial -> devices[0] (peer copy over xGMI), ordered on this device's stream
     HIPCHK(hipMemcpyPeerAsync(root->gather + k * OVH_PARTIAL_BYTES, s0->device, s->part_out, s->device,
@@ -1527,6 +1551,10 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   if (!c) return nullptr;
   c->device = device;
   c->flags = flags;
+  if (const char* e = getenv("OVH_FOLD_SIDE")) c->fold_side = atoi(e) != 0;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+    c->wg_cap = 4u * (uint32_t)ncu;
   if (!dst) {
     dst = DEFAULT_DST;
     dst_len = 43;
@@ -1537,8 +1565,8 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->part_out, 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
+            hipMalloc(&c->vstart, 8) == hipSuccess && hipMemset(c->vstart, 0, 8) == hipSuccess &&
             hipMemset(c->result, 0, 64) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
   // two finals in flight at most (LDS budget below: four vote workgroups and two finals fit a
@@ -1547,10 +1575,8 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k) c->fs[k] = c->fstream;
   for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k)
     ok = hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) == hipSuccess &&
-         hipEventCreateWithFlags(&c->ev_h[k], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_back[k], hipEventDisableTiming) == hipSuccess;
   for (int k = 0; ok && k < 4; ++k) ok = hipEventCreateWithFlags(&c->ev_x[k], hipEventDisableTiming) == hipSuccess;
-  ok = ok && hipEventCreateWithFlags(&c->ev_vote, hipEventDisableTiming) == hipSuccess;
   if (ok && (flags & OVH_FLAG_PROFILE))
     for (int k = 0; ok && k < OVH_NSTAGES; ++k)
       ok = hipEventCreate(&c->ev0[k]) == hipSuccess && hipEventCreate(&c->ev1[k]) == hipSuccess;
@@ -1593,31 +1619,28 @@ ovh_ctx* ovh_create_multi(const int* devices, int ndev, const uint8_t* dst, size
 
 static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
-  for (hipStream_t s : {c->stream, c->hstream})
-    if (s) (void)hipStreamSynchronize(s);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (hipStream_t s : {c->fstream, c->fstream2})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k]})
       if (p) (void)hipFree(p);
-  for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vm_consts,
+  for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vstart, (void*)c->vm_consts,
                   (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
                   (void*)c->tab.planes, (void*)c->tab.flags, (void*)c->qc_buf, (void*)c->qt_buf, (void*)c->gather,
                   (void*)c->mfin})
     if (p) (void)hipFree(p);
   for (void* p : c->vm_bufs) (void)hipFree(p);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
-    for (hipEvent_t e : {c->ev_front[k], c->ev_h[k], c->ev_back[k]})
+    for (hipEvent_t e : {c->ev_front[k], c->ev_back[k]})
       if (e) (void)hipEventDestroy(e);
   for (int k = 0; k < 4; ++k)
     if (c->ev_x[k]) (void)hipEventDestroy(c->ev_x[k]);
-  if (c->ev_vote) (void)hipEventDestroy(c->ev_vote);
   for (int k = 0; k < OVH_NSTAGES; ++k) {
     if (c->ev0[k]) (void)hipEventDestroy(c->ev0[k]);
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
   }
-  for (hipStream_t s : {c->stream, c->hstream})
-    if (s) (void)hipStreamDestroy(s);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   for (hipStream_t s : {c->fstream, c->fstream2})
     if (s) (void)hipStreamDestroy(s);
   delete c;
@@ -1739,7 +1762,7 @@ int ovh_verify(ovh_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* ha
     CHK(ensure_cap(s, 1));
     int slot;
     CHK(take_slot(s, &slot));
-    CHK(batch_front(s, slot, 1, d, d + 96, key, dc, false));
+    CHK(batch_front(s, slot, 1, d, d + 96, key, dc));
     CHK(enqueue_msm(s, s->stream, slot, 1, dc));
     enqueue_final(s, s->stream, region_F(s, slot, 1), region_S(s, slot, 1), 1, s->result, msm_S(s, slot));
     HIPCHK(hipGetLastError());
@@ -2192,7 +2215,7 @@ int ovh_verify_batch_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, c
   if (n == 0) return 0;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  return verify_async_locked(c, n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes);
+  return verify_async_locked(c, n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, true);
 }
 
 int ovh_batch_wait(ovh_ctx* c) {
@@ -2235,7 +2258,7 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   CHK(ensure_cap(c, n));
   int slot;
   CHK(take_slot(c, &slot));
-  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false));
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes));
   CHK(shard_partial(c, slot, (uint32_t)n, d_codes, (uint32_t*)d_partial, st));
   if (st) {
     HIPCHK(hipEventRecord(c->ev_x[1], c->stream));
