@@ -22,6 +22,8 @@ SIGNATURES = [
     ("ovh_device_count", ctypes.c_int, [_vp]),
     ("ovh_stream", _vp, [_vp]),
     ("ovh_sm3", ctypes.c_int, [_u8p, _sz, _u8p]),
+    ("ovh_vote_digests_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("ovh_vote_digests", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("ovh_sk_parse", ctypes.c_int, [_vp, _u8p, _sz, _u8p]),
     ("ovh_sign", ctypes.c_int, [_vp, _u8p, _sz, _u8p, _sz, _u8p]),
     ("ovh_sk_to_pk", ctypes.c_int, [_vp, _u8p, _sz, _u8p]),

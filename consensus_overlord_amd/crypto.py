@@ -199,6 +199,27 @@ class ConsensusCrypto:
         raise_for(self.lib.ovh_verify_aggregated(self.ctx.ptr, a, len(a), h, len(h), vd, vl, len(voters)))
 
     # ---- extensions ----
+    def vote_digests(self, votes) -> List[bytes]:
+        """hash(rlp(Vote)) of many votes on the device (ovh_vote_digests: overlord Vote RLP +
+        SM3, consensus.rs:169-175, util.rs:83-87). votes: (height, round, vote_type,
+        block_hash) tuples, block_hash <= 64 bytes (empty for a nil vote)."""
+        n = len(votes)
+        if n == 0:
+            return []
+        h = np.array([v[0] for v in votes], dtype=np.uint64)
+        r = np.array([v[1] for v in votes], dtype=np.uint64)
+        t = np.array([v[2] for v in votes], dtype=np.uint8)
+        lens = np.array([len(v[3]) for v in votes], dtype=np.uint8)
+        if any(len(v[3]) > 64 for v in votes):
+            raise ValueError("block hashes of up to 64 bytes")
+        bh = np.zeros((n, 64), dtype=np.uint8)
+        for i, v in enumerate(votes):
+            bh[i, :len(v[3])] = np.frombuffer(bytes(v[3]), dtype=np.uint8)
+        out = np.zeros((n, 32), dtype=np.uint8)
+        ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)   # noqa: E731
+        raise_for(self.lib.ovh_vote_digests(self.ctx.ptr, n, ptr(h), ptr(r), ptr(t), ptr(bh), ptr(lens), ptr(out)))
+        return [out[i].tobytes() for i in range(n)]
+
     def aggregate_public_keys(self, voters: Sequence[bytes]) -> bytes:
         """BlsPublicKey::aggregate (consensus.rs:371) -> 48-byte compressed."""
         vd, vl = _concat(voters)

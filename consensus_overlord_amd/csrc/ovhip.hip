@@ -39,6 +39,7 @@
 #include "bls/verify.hpp"
 #include "fpvm.hpp"
 #include "keygen.hpp"
+#include "rlp.hpp"
 #include "sm3.hpp"
 #include "vm_progs.inc"
 static_assert(VM_KZERO == ovh::vm::KZERO && VM_KTAB == ovh::vm::KTAB, "fixed constants (tools/fpvm/gen.py)");
@@ -133,6 +134,21 @@ __device__ __forceinline__ uint64_t rlc_scalar(uint64_t seed, uint64_t i) {
 }
 
 // ------------------------------------------------------------------------ kernels
+// Vote digests (ovh_vote_digests*): lane per vote, rlp(Vote) + SM3 (rlp.hpp, sm3.hpp).
+__global__ __launch_bounds__(WG) void k_vote_digest(uint32_t n, const uint64_t* __restrict__ heights,
+                                                    const uint64_t* __restrict__ rounds,
+                                                    const uint8_t* __restrict__ types, const uint8_t* __restrict__ bh,
+                                                    const uint8_t* __restrict__ lens, uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  uint8_t h[VOTE_HASH_MAX];
+  const uint32_t len = lens[i];
+  for (uint32_t k = 0; k < len; ++k) h[k] = bh[(size_t)i * VOTE_HASH_MAX + k];
+  uint8_t d[32];
+  vote_digest(d, heights[i], rounds[i], types[i], h, len);
+  for (int k = 0; k < 32; ++k) out[(size_t)i * 32 + k] = d[k];
+}
+
 __global__ __launch_bounds__(WG) void k_h2f(uint32_t n, const uint8_t* __restrict__ hashes, XmdTemplates t, Slab s) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n) return;
@@ -1694,6 +1710,55 @@ void* ovh_stream(ovh_ctx* c) {
 int ovh_sm3(const uint8_t* msg, size_t len, uint8_t out[32]) {
   if ((!msg && len) || !out) return OVH_ERR_ARG;
   sm3_digest(msg, len, out);
+  return 0;
+}
+
+static_assert(OVH_VOTE_HASH_MAX == VOTE_HASH_MAX, "vote hash stride");
+
+int ovh_vote_digests_device(ovh_ctx* c, size_t n, const uint64_t* heights, const uint64_t* rounds,
+                            const uint8_t* vote_types, const uint8_t* block_hashes, const uint8_t* hash_lens,
+                            uint8_t* digests) {
+  if (!c || n > (1u << 24) || (n && (!heights || !rounds || !vote_types || !block_hashes || !hash_lens || !digests)))
+    return OVH_ERR_ARG;
+  if (n == 0) return 0;
+  ovh_ctx* s = c->sub.empty() ? c : c->sub[0];
+  std::lock_guard<std::mutex> g(s->mu);
+  HIPCHK(hipSetDevice(s->device));
+  k_vote_digest<<<nblk(n), WG, 0, s->stream>>>((uint32_t)n, heights, rounds, vote_types, block_hashes, hash_lens,
+                                               digests);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ovh_vote_digests(ovh_ctx* c, size_t n, const uint64_t* heights, const uint64_t* rounds, const uint8_t* vote_types,
+                     const uint8_t* block_hashes, const uint8_t* hash_lens, uint8_t* digests) {
+  if (!c || n > (1u << 24) || (n && (!heights || !rounds || !vote_types || !block_hashes || !hash_lens || !digests)))
+    return OVH_ERR_ARG;
+  if (n == 0) return 0;
+  for (size_t i = 0; i < n; ++i)
+    if (hash_lens[i] > OVH_VOTE_HASH_MAX) return OVH_ERR_ARG;
+  ovh_ctx* s = pick_sub(c);
+  std::lock_guard<std::mutex> g(s->mu);
+  HIPCHK(hipSetDevice(s->device));
+  // staging: heights, rounds (8 B), types, lens (1 B), hashes (64 B), digests (32 B) per vote
+  const size_t per = 8 + 8 + 1 + 1 + OVH_VOTE_HASH_MAX + 32;
+  CHK(ensure_in(s, n * per + 256));
+  uint8_t* d = s->in_buf;
+  uint64_t* dh = (uint64_t*)d;
+  uint64_t* dr = dh + n;
+  uint8_t* dt = (uint8_t*)(dr + n);
+  uint8_t* dl = dt + n;
+  uint8_t* db = dl + n;
+  uint8_t* dd = db + n * OVH_VOTE_HASH_MAX;
+  HIPCHK(hipMemcpyAsync(dh, heights, n * 8, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(hipMemcpyAsync(dr, rounds, n * 8, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(hipMemcpyAsync(dt, vote_types, n, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(hipMemcpyAsync(dl, hash_lens, n, hipMemcpyHostToDevice, s->stream));
+  HIPCHK(hipMemcpyAsync(db, block_hashes, n * OVH_VOTE_HASH_MAX, hipMemcpyHostToDevice, s->stream));
+  k_vote_digest<<<nblk(n), WG, 0, s->stream>>>((uint32_t)n, dh, dr, dt, db, dl, dd);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(digests, dd, n * 32, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
   return 0;
 }
 

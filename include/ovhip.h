@@ -73,6 +73,20 @@ void* ovh_stream(ovh_ctx* ctx);
 /* Crypto::hash -> util.rs:83-87 sm3_hash. */
 int ovh_sm3(const uint8_t* msg, size_t len, uint8_t out[32]);
 
+/* Vote digests on the device: digest i = SM3(rlp(Vote{height, round,
+ * vote_type, block_hash})), the hash overlord signs and Consensus::check_block rebuilds
+ * (consensus.rs:169-175 -> util.rs:83-87), so the batching shim can ship raw votes and feed the
+ * digests straight to ovh_verify_batch_device. Vote i's block hash is the first hash_lens[i]
+ * (<= OVH_VOTE_HASH_MAX; 0 = the empty hash of a nil vote) bytes at block_hashes + 64 i.
+ * _device: every pointer is device memory, the kernel is enqueued on ovh_stream and the call
+ * returns without waiting (stream order). Host form: host buffers, synchronous. */
+#define OVH_VOTE_HASH_MAX 64
+int ovh_vote_digests_device(ovh_ctx* ctx, size_t n, const uint64_t* heights, const uint64_t* rounds,
+                            const uint8_t* vote_types, const uint8_t* block_hashes, const uint8_t* hash_lens,
+                            uint8_t* digests);
+int ovh_vote_digests(ovh_ctx* ctx, size_t n, const uint64_t* heights, const uint64_t* rounds, const uint8_t* vote_types,
+                     const uint8_t* block_hashes, const uint8_t* hash_lens, uint8_t* digests);
+
 /* BlsPrivateKey::try_from (consensus.rs:349-350, ophelia-blst [dep]): the 32-byte scalar the
  * context signs with, big-endian. Default: IETF KeyGen (blst SecretKey::key_gen(key, ""):
  * HKDF-SHA256, key >= 32 bytes) -- the reference's own example/private_key is >= r, so the

@@ -4,12 +4,21 @@
 #include <string.h>
 #include "../../consensus_overlord_amd/csrc/bls/verify.hpp"
 #include "../../consensus_overlord_amd/csrc/fpvm.hpp"
+#include "../../consensus_overlord_amd/csrc/rlp.hpp"
 
 using namespace ovh;
 
 static const uint8_t DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_";
 
 extern "C" {
+
+// rlp(Vote) + SM3 of rlp.hpp (the k_vote_digest code) on the host
+int hx_vote_rlp(uint8_t* out, uint64_t h, uint64_t r, uint8_t t, const uint8_t* bh, uint32_t bl) {
+  return (int)rlp_vote(out, h, r, t, bh, bl);
+}
+void hx_vote_digest(uint8_t* out32, uint64_t h, uint64_t r, uint8_t t, const uint8_t* bh, uint32_t bl) {
+  vote_digest(out32, h, r, t, bh, bl);
+}
 
 int hx_hash_to_g2(const uint8_t* msg32, const uint8_t* dst, uint32_t dst_len, uint8_t* out192) {
   XmdTemplates t;
