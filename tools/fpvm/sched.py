@@ -81,7 +81,7 @@ class Scheduled:
 
 
 def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1, mixed=True, slot_target=None,
-             hoist=None, stretch=1.3, split_sop=False, dual=False, bias=None):
+             hoist=None, stretch=1.3, split_sop=False, dual=False, bias=None, light_margin=0):
     ops = prog.ops
     live = prog.live_ops()
     liveset = set(live)
@@ -166,7 +166,7 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
         if dual:   # every lane runs one heavy and one light op per phase
             kind = "H" if eh else "L"
             cur = pick(eh, W, pressure) + pick(el, W, pressure)
-        elif top_l > top_h or not eh:
+        elif top_l > top_h + light_margin or not eh:
             kind = "L"
             cur = pick(el, W, pressure)
         else:
