@@ -1322,6 +1322,22 @@ static void enqueue_bisect(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, int
 
 // One batch, pipelined: per-vote stages + wide fold levels on the main stream; the narrow fold
 // levels, the combined check and the gated bisection on the final stream. Caller holds c->mu.
+// The final stream of `slot` after the vote kernel (batch_front without fold level 1): waits for
+// it, with `pipe` also for the next batch's vote workgroups to be resident (k_gate), then the
+// fold levels R0 -> R1 -> ... down to <= until partials (*reg, *m).
+static int side_front(ovh_ctx* c, int slot, uint32_t n, bool pipe, uint32_t until, int* reg, uint32_t* m) {
+  hipStream_t fst = c->fs[slot];
+  HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
+  HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
+  const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
+  if (pipe) k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
+  *m = groups_of(n);
+  *reg = 1;
+  k_vm_fold<VM_FOLD_UNITS><<<(*m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, fst>>>(
+      nwg, c->vm_fold, c->vm_consts, region_F(c, slot, 0), region_S(c, slot, 0), region_F(c, slot, 1), nullptr);
+  return fold_down(c, slot, fst, VM_SLICES, reg, m, until);
+}
+
 // pipe (ovh_verify_batch_device_async): the final stream first waits (k_gate) until the next
 // batch's vote workgroups are resident.
 static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
@@ -1334,21 +1350,18 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
   hipStream_t fst = c->fs[slot];
   uint32_t m = groups_of((uint32_t)n);
   int reg = 1;
-  const uint32_t nwg = ((uint32_t)n + VM_SLICES - 1) / VM_SLICES;
   if (side) {  // fold levels on the final stream, beside the next batch's vote kernel
-    HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
-    HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
-    if (pipe) k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
-    k_vm_fold<VM_FOLD_UNITS><<<(m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, fst>>>(
-        nwg, c->vm_fold, c->vm_consts, region_F(c, slot, 0), region_S(c, slot, 0), region_F(c, slot, 1), nullptr);
-    CHK(fold_down(c, slot, fst, VM_SLICES, &reg, &m, 4));
+    CHK(side_front(c, slot, (uint32_t)n, pipe, 4, &reg, &m));
   } else {
     // every fold level on the main stream (it idles while a final runs): the final streams carry
     // only the MSM, the finals and the bisections
     CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 4));
     HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
     HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
-    if (pipe) k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
+    if (pipe) {
+      const uint32_t nwg = ((uint32_t)n + VM_SLICES - 1) / VM_SLICES;
+      k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
+    }
   }
   int32_t* verdict = c->result + RES_BATCH + slot;
   CHK(enqueue_msm(c, fst, slot, (uint32_t)n, d_codes));
@@ -2323,14 +2336,28 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   CHK(ensure_cap(c, n));
   int slot;
   CHK(take_slot(c, &slot));
-  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes));
-  CHK(shard_partial(c, slot, (uint32_t)n, d_codes, (uint32_t*)d_partial, st));
-  if (st) {
-    HIPCHK(hipEventRecord(c->ev_x[1], c->stream));
-    HIPCHK(hipStreamWaitEvent(st, c->ev_x[1], 0));
+  if (!st) {
+    CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes));
+    CHK(shard_partial(c, slot, (uint32_t)n, d_codes, (uint32_t*)d_partial, nullptr));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
   }
-  HIPCHK(hipStreamSynchronize(c->stream));
+  // pipelined: only hash_to_field + the vote kernel on the main stream; the fold levels, the MSM
+  // and the packing on the slot's final stream (behind the residency gate), which the caller's
+  // stream then waits for (its all-gather, then ovh_combine_partials_device_async)
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false));
+  hipStream_t fst = c->fs[slot];
+  int reg;
+  uint32_t m;
+  CHK(side_front(c, slot, (uint32_t)n, true, 1, &reg, &m));
+  CHK(enqueue_msm(c, fst, slot, (uint32_t)n, d_codes));
+  HIPCHK(hipEventRecord(c->ev_x[0], st));  // the caller's earlier work (a gather out of d_partial)
+  HIPCHK(hipStreamWaitEvent(fst, c->ev_x[0], 0));
+  k_pack_partial2<<<1, 64, 0, fst>>>(region_F(c, slot, reg), msm_S(c, slot), (uint32_t*)d_partial);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev_x[1], fst));
+  HIPCHK(hipStreamWaitEvent(st, c->ev_x[1], 0));
+  HIPCHK(hipEventRecord(c->ev_back[slot], fst));  // (ovh_batch_fallback_device waits for it)
   return 0;
 }
 
@@ -2401,6 +2428,7 @@ int ovh_batch_fallback_device(ovh_ctx* c, size_t n, int32_t* d_codes) {
   HIPCHK(hipSetDevice(c->device));
   if (n == 0) return 0;
   if (n != c->last_n || c->slot_n[c->last_slot] != n) return OVH_ERR_ARG;
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_back[c->last_slot], 0));  // the slot's final-stream work
   enqueue_bisect(c, c->stream, c->last_slot, (uint32_t)n, d_codes, nullptr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
