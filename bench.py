@@ -36,6 +36,12 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# Hardware queues per process (HIP's default is 4). libovhip runs three streams (per-vote stages,
+# two final streams); torch's stream and the process group's RCCL stream come on top at N > 1.
+# With four queues two of those streams share one queue and run in order, which put the
+# final-stream work of the multi-GPU path back in line with the vote kernels (r02ae trace:
+# 814k instead of 1,008k verifs/s at one rank). Set before HIP initialises (torch import).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 sys.path.insert(0, ROOT)
 
 SEED = 0xC17A
@@ -203,6 +209,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the untimed latency probes")
+    ap.add_argument("--shard-path", action="store_true",
+                    help="diagnostic: run the multi-GPU pipeline (partials + RCCL all-gather) even at N=1")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -220,6 +228,10 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif args.shard_path:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
     ctx = Context(local, flags=OVH_FLAG_PROFILE)
     lib = ctx.lib
     B = args.batch
@@ -232,7 +244,7 @@ def main():
     sigs = dev.sign_batch(ctx, sks, hs)
     nbatch = args.warmup + args.steps + args.profile_steps
     codes = torch.full((nbatch, B), -1, dtype=torch.int32, device="cuda")   # one verdict row per batch
-    shards = ShardVerifier(DeviceBackend(ctx)) if world > 1 else None
+    shards = ShardVerifier(DeviceBackend(ctx)) if (world > 1 or args.shard_path) else None
     torch.cuda.synchronize()
 
     nst = NSTAGES
@@ -250,7 +262,7 @@ def main():
         """Enqueue batch s. Pipelined: batch s's combined check / bisection (second stream)
         overlaps batch s + 1's per-vote stages; every batch's codes row is final after
         batch_wait. Each batch's RLC coefficients come from a fresh getrandom seed (library)."""
-        if world == 1:
+        if shards is None:
             dev.verify_batch_async(ctx, sigs, hs, pks, codes[s])
         else:
             shards.submit(s, sigs, hs, pks, codes[s], index_base=rank * B)
@@ -339,7 +351,7 @@ def main():
             "data": "synthetic (seed 0xC17A keypairs + RLP precommit votes, SURVEY.md 8(d))",
             "config": {"workload": "config3: %d distinct-message precommit votes per GPU, RLC batch verify" % B,
                        "batch_per_gpu": B, "global_batch": world * B,
-                       "parallelism": "vote shards x%d, partials all-gathered over RCCL" % world if world > 1
+                       "parallelism": "vote shards x%d, partials all-gathered over RCCL" % world if shards is not None
                        else "single GPU"},
             "roofline": {
                 "bound": "valu",
@@ -370,7 +382,7 @@ def main():
             line["cpu_baseline"] = cpu_baseline(sigs.cpu().numpy(), hs_h, pks.cpu().numpy(), args.cpu_seconds)
         print(json.dumps(line), flush=True)
     ctx.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

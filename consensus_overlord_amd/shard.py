@@ -36,15 +36,19 @@ class DeviceBackend:
         from . import device
         self.ctx = ctx
         self.dev = device
+        # the gather's stream: a stream of its own, never torch's default (null) stream, whose
+        # handle 0 would ask libovhip for the synchronous partial (include/ovhip.h) and put the
+        # fold levels, the MSM and the packing back in line with the vote kernels
+        self.stream = torch.cuda.Stream()
 
     def empty_partials(self, world: int) -> torch.Tensor:
         return torch.empty((BATCH_SLOTS, world, PARTIAL_BYTES), dtype=torch.uint8, device="cuda")
 
     def partial(self, sigs, hashes, pks, codes, out_row, index_base: int) -> None:
-        self.dev.batch_partial(self.ctx, sigs, hashes, pks, codes, out_row, stream=True)
+        self.dev.batch_partial(self.ctx, sigs, hashes, pks, codes, out_row, stream=self.stream)
 
     def combine_async(self, parts, n: int, codes) -> None:
-        self.dev.combine_partials_async(self.ctx, parts, n, codes, stream=True)
+        self.dev.combine_partials_async(self.ctx, parts, n, codes, stream=self.stream)
 
     def wait(self) -> None:
         self.dev.batch_wait(self.ctx)
@@ -73,6 +77,15 @@ class ShardVerifier:
         all-gather -> combined check and (device-gated) bisection into `codes`, final after
         wait()."""
         part = self.partials[s % self.partials.shape[0]]
+        st = getattr(self.backend, "stream", None)
+        if st is not None:
+            st.wait_stream(torch.cuda.current_stream())   # the caller's inputs
+            with torch.cuda.stream(st):
+                self._submit(part, sigs, hashes, pks, codes, index_base)
+        else:
+            self._submit(part, sigs, hashes, pks, codes, index_base)
+
+    def _submit(self, part, sigs, hashes, pks, codes, index_base):
         self.backend.partial(sigs, hashes, pks, codes, part[self.rank], index_base)
         self._all_gather(part)
         self.backend.combine_async(part, sigs.shape[0], codes)
