@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void k_msm_count(uint32_t n, uint64_t seed, ui
   __syncthreads();
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i < n && codes[i] == 0) {  // failed votes contribute the identity
-    const uint64_t r = rlc_scalar(seed, base + i);
+    const uint64_t r = vote_scalar(seed, base, i);
     for (uint32_t hh = 0; hh < 2; ++hh) {
       const uint32_t s = msm_half(r, hh);
       for (uint32_t w = 0; w < 4; ++w) {
@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void k_msm_scatter(uint32_t n, uint64_t seed, 
                                                      uint32_t* __restrict__ ent) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n || codes[i] != 0) return;
-  const uint64_t r = rlc_scalar(seed, base + i);
+  const uint64_t r = vote_scalar(seed, base, i);
   for (uint32_t hh = 0; hh < 2; ++hh) {
     const uint32_t s = msm_half(r, hh);
     for (uint32_t w = 0; w < 4; ++w) {
@@ -114,6 +114,18 @@ __global__ __launch_bounds__(256) void k_msm_scatter(uint32_t n, uint64_t seed, 
       if (d) ent[atomicAdd(&cur[w * MSM_NBW + d - 1], 1u)] = 2 * i + hh;
     }
   }
+}
+
+// single-vote batch (UNIT_BASE): S = sigma (affine -> (x : y : 1)), or O if the vote failed
+__global__ __launch_bounds__(64) void k_sig_as_S(Slab st, const int32_t* __restrict__ codes, Slab U) {
+  const uint32_t c = threadIdx.x;
+  if (c >= 6) return;
+  Fp v;
+  const bool ok = codes[0] == 0;
+  if (ok && c < 4) st.ld(v, S_SIG + c, 0);
+  else if (c == (ok ? 4u : 2u)) fp_one(v);
+  else fp_zero(v);
+  U.st(v, c, 0);
 }
 
 enum : uint32_t { MSM_L0 = 0, MSM_LVL = 1, MSM_T0 = 2, MSM_TL = 3, MSM_HRN = 4 };

@@ -133,6 +133,14 @@ __device__ __forceinline__ uint64_t rlc_scalar(uint64_t seed, uint64_t i) {
   return z ? z : 1;
 }
 
+// A batch of one vote checks its own pairing equation, e(pk, H) e(-G1, sigma) = 1: no random
+// coefficient is needed, so its scalar is 1 (base UNIT_BASE) and the "MSM" is sigma itself
+// (k_sig_as_S), which saves the MSM's launches on the per-call path (ovh_verify).
+#define UNIT_BASE 0xFFFFFFFFFFFFFFFFull
+__device__ __forceinline__ uint64_t vote_scalar(uint64_t seed, uint64_t base, uint64_t i) {
+  return base == UNIT_BASE ? 1ull : rlc_scalar(seed, base + i);
+}
+
 // ------------------------------------------------------------------------ kernels
 // Vote digests (ovh_vote_digests*): lane per vote, rlp(Vote) + SM3 (rlp.hpp, sm3.hpp).
 __global__ __launch_bounds__(WG) void k_vote_digest(uint32_t n, const uint64_t* __restrict__ heights,
@@ -323,7 +331,7 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
   }
   __syncthreads();
   vote_stagger();
-  vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
+  vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, vote_scalar(seed, base, i),
           vm::Out{s.p, s.cap, i},
           blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) {
@@ -465,7 +473,7 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
   }
   __syncthreads();
   vote_stagger();
-  vm::run(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
+  vm::run(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst, vote_scalar(seed, base, i),
           vm::Out{s.p, s.cap, i}, blockIdx.x == 0 ? prog.trace : nullptr);
   if (active && lane == 0) {
     const uint32_t sf = hdr[0], pf = hdr[1];
@@ -568,7 +576,7 @@ __global__ __launch_bounds__(64) void k_vm_rs(uint32_t n, VmDev prog, const uint
     slot_put(slots, VM_RS_IN[lane], v.v);
   }
   __syncthreads();
-  vm::run(prog.code, VM_RS_NPHASES, VM_RS_W, lane, active, slots, cst, rlc_scalar(seed, base + i),
+  vm::run(prog.code, VM_RS_NPHASES, VM_RS_W, lane, active, slots, cst, vote_scalar(seed, base, i),
           vm::Out{s.p, s.cap, i});
 }
 
@@ -1186,14 +1194,19 @@ struct KeySrc {
 };
 
 // Per-vote stages of a batch in `slot`: hash_to_field, the vote kernel with fold level 0 fused
-// (-> R0), fold level 1 (-> R1: one partial per 16-vote group, kept for the bisection).
+// (-> R0), fold level 1 (-> R1: one partial per 16-vote group). alone: the batch's combined
+// check covers only this batch (not a shard of a larger combined check).
 static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
-                       int32_t* d_codes, bool fold1 = true) {
+                       int32_t* d_codes, bool fold1 = true, bool alone = false) {
   Slab s{c->state_slot[slot], c->cap};
   hipStream_t st = c->stream;
   c->ev_mask = 0;
   uint64_t seed, base;
   CHK(draw_seed(c, &seed, &base));
+  // one vote checked on its own (alone: never combined with other partials): its pairing
+  // equation needs no random coefficient, scalar 1 (vote_scalar). A one-vote shard keeps its
+  // random scalar: its partial is combined with the other shards'.
+  if (n == 1 && alone) base = UNIT_BASE;
   c->slot_seed[slot] = seed;
   c->slot_base[slot] = base;
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
@@ -1267,6 +1280,10 @@ static int enqueue_msm(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, const i
   uint32_t* cur;
   const MsmArgs a = msm_args(c, slot, &cur);
   const uint64_t seed = c->slot_seed[slot], base = c->slot_base[slot];
+  if (base == UNIT_BASE) {  // a single vote with scalar 1: S = sigma
+    k_sig_as_S<<<1, 64, 0, st>>>(a.st, d_codes, a.U);
+    return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
+  }
   uint32_t nlev = 1;  // tree levels: 2^nlev >= the largest possible bucket (2n points)
   while ((1ull << nlev) < 2ull * n) ++nlev;
   if (nlev > MSM_LV) return OVH_ERR_ARG;
@@ -1346,7 +1363,7 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
   int slot;
   CHK(take_slot(c, &slot));
   const bool side = c->fold_side;
-  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, !side));
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, !side, true));
   hipStream_t fst = c->fs[slot];
   uint32_t m = groups_of((uint32_t)n);
   int reg = 1;
@@ -1840,7 +1857,7 @@ int ovh_verify(ovh_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* ha
     CHK(ensure_cap(s, 1));
     int slot;
     CHK(take_slot(s, &slot));
-    CHK(batch_front(s, slot, 1, d, d + 96, key, dc));
+    CHK(batch_front(s, slot, 1, d, d + 96, key, dc, true, true));
     CHK(enqueue_msm(s, s->stream, slot, 1, dc));
     enqueue_final(s, s->stream, region_F(s, slot, 1), region_S(s, slot, 1), 1, s->result, msm_S(s, slot));
     HIPCHK(hipGetLastError());

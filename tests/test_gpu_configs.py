@@ -120,3 +120,30 @@ def test_rlc_cancellation_needs_known_seed():
     assert t.verify_batch(sigs, hs, pks).tolist() == [0, 0, 0, 0]
     t.ctx.set_test_rlc(seed + 1, 0)
     assert t.verify_batch(sigs, hs, pks).tolist() == [5, 0, 5, 0]
+
+
+def test_unit_scalar_only_for_a_standalone_vote():
+    """A batch of one vote checks its own pairing equation with scalar 1 (ovhip.hip
+    vote_scalar / k_sig_as_S); a one-vote shard of a larger combined check must keep its random
+    coefficient: sigma_0 + T and sigma_1 - T (cancelling under unit scalars) split over a
+    two-device context are both flagged, and each alone verifies to 5."""
+    import consensus_overlord_amd as coa
+    from consensus_overlord_amd.crypto import Context
+    from rlc_attack import bls
+    with open(os.path.join(ROOT, "tests", "golden", "golden_v1.json")) as fh:
+        g = json.load(fh)
+    sigs = [bytes.fromhex(x["sig"]) for x in g["votes"][:2]]
+    hs = [bytes.fromhex(x["digest"]) for x in g["votes"][:2]]
+    pks = [bytes.fromhex(x["pk"]) for x in g["keys"][:2]]
+    F, T = bls.Fp2Ops, bls.G2_GEN
+    forged = [bls.g2_compress(bls.pt_add(F, bls.g2_from_bytes(sigs[0]), T)),
+              bls.g2_compress(bls.pt_add(F, bls.g2_from_bytes(sigs[1]), bls.pt_neg(F, T)))]
+    one = coa.ConsensusCrypto(bytes.fromhex("55" * 32))
+    assert one.verify_batch(sigs[:1], hs[:1], pks[:1]).tolist() == [0]
+    for k in range(2):
+        assert one.verify_batch(forged[k:k + 1], hs[k:k + 1], pks[k:k + 1]).tolist() == [5]
+        assert one.lib.ovh_verify(one.ctx.ptr, forged[k], 96, hs[k], 32, pks[k], 48) == 5
+    multi = coa.ConsensusCrypto(bytes.fromhex("55" * 32), ctx=Context(devices=[0, 0]))
+    for _ in range(3):
+        assert multi.verify_batch(forged, hs, pks).tolist() == [5, 5]
+        assert multi.verify_batch(sigs, hs, pks).tolist() == [0, 0]
