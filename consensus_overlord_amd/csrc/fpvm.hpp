@@ -487,7 +487,11 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
   Fp A, B, C, D;
   ld_slots4(A, B, C, D, slots, cst, ra, rb, rc, in.z >> 16);
   const bool is_mul = op == OP_MULS || op == OP_SGN0 || op == OP_LEX || op == OP_EQ;
+#ifndef OVH_VM_UNIT_LIN
+  const bool lin_unit = false;  // every lin op runs lin_mad (tools/fpvm/sched.py ALL_ACC)
+#else
   const bool lin_unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1;
+#endif
   const bool is_lin = (op == OP_LIN && lin_unit) || selb;
   const bool is_acc = op == OP_LIN && !lin_unit;
   if (hdr & H_MUL) {

@@ -152,6 +152,9 @@ def _beta():
 BETA = _beta()
 
 
+JAC_COFACTOR = True   # cofactor clearing's [|x|] chains in Jacobian coordinates (see g2_jac_dbl)
+
+
 class Alg:
     def __init__(self, prog: Prog, inv_op: bool = False, use_sop: bool = False):
         self.p = prog
@@ -783,16 +786,78 @@ class Alg:
         Y = self.f2_mul(self.f2_mul(y, YN), xdXD2)
         return (X, Y, Z)
 
+    # Jacobian (x = X/Z^2, y = Y/Z^3) chains for cofactor clearing only: dbl-2009-l doubling
+    # (a = 0) is 3 product levels deep against ~5 for the complete homogeneous formula, so the
+    # two 63-doubling chains of h_eff, which sit on the vote program's critical path, shorten.
+    # The additions (add-2007-bl) are not complete: they fail only when an intermediate [k]A
+    # equals +-A, i.e. when the hash point's order is below 2^64 -- never, for a point derived
+    # from a hash. Subgroup checks keep the complete formulas (their inputs are adversarial).
+    def _f2_lin(self, terms):
+        p = self.p
+        return (p.lin([(c, v[0]) for c, v in terms]), p.lin([(c, v[1]) for c, v in terms]))
+
+    def g2_hom_to_jac(self, A):
+        X, Y, Z = A
+        return (self.f2_mul(X, Z), self.f2_mul(Y, self.f2_sqr(Z)), Z)
+
+    def g2_jac_to_hom(self, A):
+        X, Y, Z = A
+        return (self.f2_mul(X, Z), Y, self.f2_mul(Z, self.f2_sqr(Z)))
+
+    def g2_jac_dbl(self, A):
+        X, Y, Z = A
+        a = self.f2_sqr(X)
+        b = self.f2_sqr(Y)
+        yz = self.f2_mul(Y, Z)
+        c = self.f2_sqr(b)
+        e1 = self.f2_sqr(self.f2_add(X, b))
+        f1 = self.f2_sqr(a)
+        X3 = self._f2_lin([(9, f1), (-4, e1), (4, a), (4, c)])
+        u = self._f2_lin([(6, e1), (-6, a), (-6, c), (-9, f1)])
+        Y3 = self._f2_lin([(3, self.f2_mul(a, u)), (-8, c)])
+        Z3 = self._f2_lin([(2, yz)])
+        return (X3, Y3, Z3)
+
+    def g2_jac_add(self, A, B):
+        X1, Y1, Z1 = A
+        X2, Y2, Z2 = B
+        z1z1 = self.f2_sqr(Z1)
+        z2z2 = self.f2_sqr(Z2)
+        u1 = self.f2_mul(X1, z2z2)
+        u2 = self.f2_mul(X2, z1z1)
+        s1 = self.f2_mul(Y1, self.f2_mul(Z2, z2z2))
+        s2 = self.f2_mul(Y2, self.f2_mul(Z1, z1z1))
+        h = self.f2_sub(u2, u1)
+        i = self.f2_sqr(self.f2_dbl(h))
+        j = self.f2_mul(h, i)
+        r = self._f2_lin([(2, s2), (-2, s1)])
+        v = self.f2_mul(u1, i)
+        X3 = self._f2_lin([(1, self.f2_sqr(r)), (-1, j), (-2, v)])
+        Y3 = self._f2_lin([(1, self.f2_mul(r, self.f2_sub(v, X3))), (-2, self.f2_mul(s1, j))])
+        Z3 = self.f2_mul(self._f2_lin([(1, self.f2_sqr(self.f2_add(Z1, Z2))), (-1, z1z1), (-1, z2z2)]), h)
+        return (X3, Y3, Z3)
+
+    def g2_mul_fixed_jac(self, A, k: int):
+        """[k] A (homogeneous in and out) by a Jacobian double-and-add chain."""
+        J = self.g2_hom_to_jac(A)
+        acc = J
+        for b in bin(k)[3:]:
+            acc = self.g2_jac_dbl(acc)
+            if b == "1":
+                acc = self.g2_jac_add(acc, J)
+        return self.g2_jac_to_hom(acc)
+
     def clear_cofactor(self, A):
         """h_eff A = [x^2 - x - 1] A + [x - 1] psi(A) + psi^2(2A), x = -X_ABS (RFC 9380 G.3).
         With t1 = [X_ABS] A and psi commuting with scalars:
           h_eff A = [X_ABS] B + K,  B = t1 - psi(A),  K = B - A + psi^2(2A),
         so only K (one point) is held across the second scalar chain."""
-        t1 = self.pt_mul_fixed("f2", A, X_ABS)
+        mul = self.g2_mul_fixed_jac if JAC_COFACTOR else (lambda P_, k: self.pt_mul_fixed("f2", P_, k))
+        t1 = mul(A, X_ABS)
         B = self.pt_add("f2", t1, self.pt_neg("f2", self.g2_psi(A)))
         K = self.pt_add("f2", self.pt_add("f2", B, self.pt_neg("f2", A)),
                         self.g2_psi(self.g2_psi(self.pt_dbl("f2", A))))
-        return self.pt_add("f2", self.pt_mul_fixed("f2", B, X_ABS), K)
+        return self.pt_add("f2", mul(B, X_ABS), K)
 
     def hash_to_g2(self, u0, u1):
         q0 = self.iso_map(*self.map_to_curve_sswu(u0))

@@ -31,6 +31,11 @@ CONST_BASE = 0x800
 ABSENT = 0xFFFF
 # LDS pass width (lanes) and slot residues that share banks (OVH_BANK="lanes,mod" for A/B builds)
 BANK_LANES, BANK_MOD = (int(x) for x in os.environ.get("OVH_BANK", "16,16").split(","))
+# every lin op in the general-coefficient form (fpvm.hpp lin_mad): one linear block per phase
+# instead of the unit-sign block plus the general one; measured faster even for unit sums with
+# negations (r02aj: 1,013k -> 1,031-1,038k verifs/s). OVH_GEN_UNITLIN=1 with an interpreter
+# built with OVH_VM_UNIT_LIN restores the unit-sign path (A/B builds).
+ALL_ACC = os.environ.get("OVH_GEN_UNITLIN", "0") != "1"
 R_MONT = pow(2, 384, P)
 
 
@@ -328,6 +333,9 @@ def lane_operands(prog, i):
             coefs = [c for c, _ in u]
             if form[0] == "scaled":
                 scale = form[1]
+                if ALL_ACC:
+                    coefs = [c * scale for c in coefs]
+                    scale = 0
         A, B, C, D = srcs[:4]
         if LW == 8:
             ext = srcs[4:8]
@@ -418,7 +426,7 @@ def phase_bits(w):
     if opc == OPC["selb"]:
         return H_LIN | H_SELB
     if opc == OPC["lin"]:
-        if ca == 1 and all(-1 <= c <= 1 for c in (cb, cc, cd)):
+        if ca == 1 and all(-1 <= c <= 1 for c in (cb, cc, cd)) and not ALL_ACC:
             return H_LIN | (H_LINNEG if min(cb, cc, cd) < 0 else 0)
         return H_ACC
     return H_RARE
