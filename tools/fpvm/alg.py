@@ -805,15 +805,23 @@ class Alg:
         return (self.f2_mul(X, Z), Y, self.f2_mul(Z, self.f2_sqr(Z)))
 
     def g2_jac_dbl(self, A):
+        """S = 4 X Y^2 as the product X (Y^2) rather than (X + Y^2)^2 - X^2 - Y^4 (dbl-2009-l):
+        one product more, but no sum ahead of a square, so the chain through Y is two products,
+        a linear combination, a product and a linear combination deep."""
         X, Y, Z = A
         a = self.f2_sqr(X)
         b = self.f2_sqr(Y)
         yz = self.f2_mul(Y, Z)
         c = self.f2_sqr(b)
-        e1 = self.f2_sqr(self.f2_add(X, b))
-        f1 = self.f2_sqr(a)
-        X3 = self._f2_lin([(9, f1), (-4, e1), (4, a), (4, c)])
-        u = self._f2_lin([(6, e1), (-6, a), (-6, c), (-9, f1)])
+        # X b by Karatsuba, its three Fp products combined straight into X3 and u (xb is used
+        # twice, so a shared post-addition would add a level)
+        p = self.p
+        t0, t1 = X[0] * b[0], X[1] * b[1]
+        t2 = p.muls(X[0], 1, X[1], b[0], 1, b[1])
+        f = self.f2_sqr(a)
+        # X3 = M^2 - 2S = 9 f - 8 xb (M = 3 X^2), u = S - X3 = 12 xb - 9 f; xb = (t0 - t1, t2 - t0 - t1)
+        X3 = (p.lin([(9, f[0]), (-8, t0), (8, t1)]), p.lin([(9, f[1]), (-8, t2), (8, t0), (8, t1)]))
+        u = (p.lin([(-9, f[0]), (12, t0), (-12, t1)]), p.lin([(-9, f[1]), (12, t2), (-12, t0), (-12, t1)]))
         Y3 = self._f2_lin([(3, self.f2_mul(a, u)), (-8, c)])
         Z3 = self._f2_lin([(2, yz)])
         return (X3, Y3, Z3)

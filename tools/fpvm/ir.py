@@ -23,6 +23,7 @@ prologue fills.
 from __future__ import annotations
 
 import math
+import os
 
 P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
 HALF_P = (P - 1) // 2
@@ -115,7 +116,11 @@ def lin_form(terms, width=None):
     return ("acc", terms)
 
 
-FORM_COST = {"unit": 1, "scaled": 2, "acc": 6}
+# fusion cost of each form: with every lin op in the general-coefficient block (sched.ALL_ACC,
+# the default) the three forms cost the same; the unit-sign interpreter path
+# (OVH_GEN_UNITLIN=1) prefers unit sums
+FORM_COST = {"unit": 1, "scaled": 2, "acc": 6} if os.environ.get("OVH_GEN_UNITLIN", "0") == "1" else \
+    {"unit": 1, "scaled": 1, "acc": 1}
 
 
 class Prog:
