@@ -316,7 +316,12 @@ class Alg:
         odd = [a]
         for _ in range((1 << (w - 1)) - 1):
             odd.append(self.f2_mul(odd[-1], sq))
-        odd_c = [self.f2_conj(t) for t in odd]
+        pp = self.p
+
+        def mul_conj(x, t):   # x * conj(t) by Karatsuba with the signs folded in (no conj slots)
+            t0, t1 = x[0] * t[0], x[1] * t[1]
+            t2 = pp.muls(x[0], 1, x[1], t[0], -1, t[1])
+            return (pp.lin([(1, t0), (1, t1)]), pp.lin([(1, t2), (-1, t0), (1, t1)]))
 
         def windows(x):   # {bit position: odd window value}, sum(v << pos) == x
             out, i = {}, x.bit_length() - 1
@@ -335,10 +340,13 @@ class Alg:
         for pos in range(max(e0.bit_length(), e1.bit_length()) - 1, -1, -1):
             if acc is not None:
                 acc = self.f2_sqr(acc)
-            for wins, tab in ((w0, odd), (w1, odd_c)):
+            for wins, cj in ((w0, False), (w1, True)):
                 if pos in wins:
-                    t = tab[wins[pos] >> 1]
-                    acc = t if acc is None else self.f2_mul(acc, t)
+                    t = odd[wins[pos] >> 1]
+                    if acc is None:
+                        acc = self.f2_conj(t) if cj else t
+                    else:
+                        acc = mul_conj(acc, t) if cj else self.f2_mul(acc, t)
         return acc
 
     def f2_sgn0(self, a):
