@@ -80,9 +80,11 @@ def build_vote():
     pk_ok, (px, py) = a.g1_decompress(pkx, p.input("pk_sort"))
     Pp = (px, py, p.one)
     pk_grp, _ = a.g1_in_group(Pp)
+    p.section = "sig"   # the signature's decompression + subgroup check (gen.py SEC_BIAS)
     sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
     Qs = (qx, qy, (p.one, p.zero))
     sig_grp = a.g2_in_group(Qs)
+    p.section = None
     H = a.hash_to_g2(u0, u1)
     h_inf = a.f2_is_zero(H[2])
     rP = a.pt_mul_glv("fp", Pp, a.g1_phi(Pp))          # projective: no inversion
@@ -106,9 +108,11 @@ def build_vote_t():
     sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
     u0 = (p.input("u00"), p.input("u01"))
     u1 = (p.input("u10"), p.input("u11"))
+    p.section = "sig"   # the signature's decompression + subgroup check (gen.py SEC_BIAS)
     sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
     Qs = (qx, qy, (p.one, p.zero))
     sig_grp = a.g2_in_group(Qs)
+    p.section = None
     H = a.hash_to_g2(u0, u1)
     h_inf = a.f2_is_zero(H[2])
     rP = a.pt_mul_glv("fp", Pp, a.g1_phi(Pp))
