@@ -277,3 +277,65 @@ class ConsensusCrypto:
         raise_for(self.lib.ovh_verify_qc_batch(self.ctx.ptr, n, sig, hs, b"".join(bytes(b) for b in bitmaps), bl,
                                                codes.ctypes.data_as(ctypes.c_void_p)))
         return codes[:n]
+
+    # ---- Consensus::check_block (consensus.rs:143-207) over the Crypto surface ----
+    def check_block(self, proposal_height: int, proposal_data: bytes, proof: bytes,
+                    authority_list: Optional[Sequence[bytes]] = None) -> bool:
+        """consensus.rs:143-207: sm3(proposal data) (:148); decode the overlord Proof (:158,
+        layout in vote.py); proof.block_hash == that hash and proof.height == proposal height
+        (:165); voters = extract_voters(authority list, bitmap) (:166-167); vote hash =
+        hash(rlp(Vote{height, round, Precommit, block_hash})) (:169-175);
+        verify_aggregated_signature(...).is_ok() (:176-183). authority_list: the brain's node
+        addresses, i.e. the validator keys (util.rs validators_to_nodes); default = the keys
+        given to update_pubkeys. Every failure returns False, as the reference does."""
+        from . import vote as _vote
+        auth = self.pubkeys if authority_list is None else [bytes(a) for a in authority_list]
+        block_hash = self.hash(proposal_data)
+        try:
+            height, round_, bh, sig, bitmap = _vote.decode_proof(proof)
+        except ValueError:
+            return False
+        if bytes(bh) != block_hash or height != proposal_height:
+            return False
+        voters = _vote.extract_voters(auth, bitmap)
+        vh = self.hash(_vote.rlp_vote(height, round_, _vote.PRECOMMIT, bh))
+        try:
+            self.verify_aggregated_signature(sig, vh, voters)
+        except ConsensusError:
+            return False
+        return True
+
+    def check_blocks(self, blocks) -> np.ndarray:
+        """Many check_block calls against the validator table (update_pubkeys) in one pass:
+        blocks = (proposal_height, proposal_data, proof) tuples -> bool[n], element j ==
+        check_block(*blocks[j]). Vote hashes come from ovh_vote_digests and the aggregated
+        signatures are checked by ovh_verify_qc_batch (bitmaps over the key-sorted table, the
+        extract_voters order), one batch per bitmap length."""
+        from . import vote as _vote
+        n = len(blocks)
+        ok = np.zeros(n, dtype=bool)
+        live = []
+        for j, (ph, data, proof) in enumerate(blocks):
+            try:
+                height, round_, bh, sig, bitmap = _vote.decode_proof(proof)
+            except ValueError:
+                continue
+            if bytes(bh) != self.hash(data) or height != ph:
+                continue
+            if len(sig) != 96 or len(bh) > 64:
+                # the QC batch takes compressed signatures only; anything else goes the scalar way
+                ok[j] = self.check_block(ph, data, proof)
+                continue
+            live.append((j, height, round_, bytes(bh), bytes(sig), bytes(bitmap)))
+        if not live:
+            return ok
+        digests = self.vote_digests([(h, r, _vote.PRECOMMIT, bh) for _, h, r, bh, _, _ in live])
+        groups = {}
+        for (j, _, _, _, sig, bm), d in zip(live, digests):
+            groups.setdefault(len(bm), []).append((j, sig, d, bm))
+        for items in groups.values():
+            codes = self.verify_qc_batch([s for _, s, _, _ in items], [d for _, _, d, _ in items],
+                                         [b for _, _, _, b in items])
+            for (j, _, _, _), c in zip(items, codes):
+                ok[j] = c == 0
+        return ok
