@@ -580,6 +580,112 @@ __global__ __launch_bounds__(64) void k_vm_rs(uint32_t n, VmDev prog, const uint
           vm::Out{s.p, s.cap, i});
 }
 
+#define GROUPCHECK_FAIL (0x100 | BLST_POINT_NOT_IN_GROUP)
+// aggregate_signatures (consensus.rs:418-444) on the VM: one 96-byte signature per 16-lane slice
+// (program "sigchk": decompression + G2 subgroup check) -> the code k_parse_sig_list gives and
+// sigma projective (Z = 1; the identity for infinity or a failure) in planes 0..5 of `pts`.
+constexpr uint32_t SIGCHK_STRIDE_W = align128w(VM_SIGCHK_NSLOTS * 12 + 4);
+__global__ __launch_bounds__(64) void k_vm_sigchk(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                  const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                                                  int gc, int32_t* __restrict__ codes, Slab pts) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / VM_SIGCHK_W, lane = threadIdx.x % VM_SIGCHK_W;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * SIGCHK_STRIDE_W;
+  uint32_t* hdr = slots + VM_SIGCHK_NSLOTS * 12;
+  const uint32_t i = blockIdx.x * (64 / VM_SIGCHK_W) + slice;
+  const bool active = i < n;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active && lane == 0) {
+    uint32_t x1[12], x0[12], bad, inf, sort, xz;
+    parse_hdr(data + off[i], 96, x1, x0, bad, inf, sort, xz);
+    slot_put(slots, VM_SIGCHK_IN[VM_SIGCHK_IN_SIG_X1], x1);
+    slot_put(slots, VM_SIGCHK_IN[VM_SIGCHK_IN_SIG_X0], x0);
+    slot_flag(slots, VM_SIGCHK_IN[VM_SIGCHK_IN_SIG_SORT], sort);
+    hdr[0] = bad | inf << 1 | xz << 2;
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_SIGCHK_NPHASES, VM_SIGCHK_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  __syncthreads();
+  if (!active) return;
+  const uint32_t pf = hdr[0];
+  int32_t c = BLST_SUCCESS;
+  bool pt = false;
+  if (pf & 1) {
+    c = BLST_BAD_ENCODING;
+  } else if (!(pf & 2)) {  // not the infinity encoding (that one is the identity)
+    if (!slot_flag_get(slots, VM_SIGCHK_OUT[VM_SIGCHK_OUT_SIG_OK])) c = BLST_POINT_NOT_ON_CURVE;
+    else if (gc && ((pf & 4) || !slot_flag_get(slots, VM_SIGCHK_OUT[VM_SIGCHK_OUT_SIG_GRP]))) c = GROUPCHECK_FAIL;
+    else pt = true;
+  }
+  for (uint32_t k = lane; k < 6; k += VM_SIGCHK_W) {
+    Fp v;
+    if (pt && k < 4) {
+      const uint32_t src = VM_SIGCHK_OUT[VM_SIGCHK_OUT_Q0 + k];
+      for (int l = 0; l < 12; ++l) v.v[l] = slots[src * 12 + l];
+      vm::canon(v, v);
+    } else if (k == (pt ? 4u : 2u)) {
+      fp_one(v);
+    } else {
+      fp_zero(v);
+    }
+    pts.st(v, k, i);
+  }
+  if (lane == 0) codes[i] = c;
+}
+
+// One level of aggregate_signatures' pairwise sum: out[q] = in[2q] + in[2q + 1] (padd, complete
+// formulas; the identity past the end), q < ceil(m / 2), one pair per 8-lane slice.
+__global__ __launch_bounds__(64) void k_vm_g2tree(uint32_t m, VmDev prog, uint32_t stride_w,
+                                                  const uint32_t* __restrict__ cst_g, Slab in, Slab out) {
+  constexpr uint32_t W = VM_PADD_W, SL = 64 / W;
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / W, lane = threadIdx.x % W;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * stride_w;
+  const uint32_t q = blockIdx.x * SL + slice;
+  const bool active = q < (m + 1) / 2;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active) {
+    for (uint32_t k = lane; k < 12; k += W) {
+      const uint32_t e = 2 * q + k / 6, c = k % 6;
+      Fp v;
+      if (e < m) in.ld(v, c, e);
+      else if (c == 2) fp_one(v);
+      else fp_zero(v);
+      slot_put(slots, prog.in[k], v.v);
+    }
+  }
+  __syncthreads();
+  vm::run(prog.code, prog.nphases, W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  if (active) {
+    for (uint32_t k = lane; k < 6; k += W) {
+      Fp v;
+      const uint32_t src = prog.out[k];
+      for (int l = 0; l < 12; ++l) v.v[l] = slots[src * 12 + l];
+      vm::canon(v, v);
+      out.st(v, k, q);
+    }
+  }
+}
+
+// projective (X : Y : Z) -> Jacobian (X Z, Y Z^2, Z) -> 96-byte compressed (one lane)
+__global__ __launch_bounds__(64) void k_g2p_compress(Slab in, uint8_t* out) {
+  if (threadIdx.x) return;
+  Fp2 X, Y, Z, zz;
+  in.ld2(X, 0, 0);
+  in.ld2(Y, 2, 0);
+  in.ld2(Z, 4, 0);
+  G2J j;
+  fp2_mul(j.X, X, Z);
+  fp2_sqr(zz, Z);
+  fp2_mul(j.Y, Y, zz);
+  j.Z = Z;
+  g2_compress(out, j);
+}
+
 #include "msm.hpp"
 
 #define GATE_TICKS 30000ull  // 300 us of the 100 MHz wall clock
@@ -691,7 +797,6 @@ __global__ __launch_bounds__(WG) void k_verify_one(const uint8_t* sig, uint32_t 
   if (threadIdx.x == 0 && blockIdx.x == 0) *out = verify_one(sig, sl, hash, hl, pk, pl, t);
 }
 
-#define GROUPCHECK_FAIL (0x100 | BLST_POINT_NOT_IN_GROUP)
 // Parse list items: code_sig[i] (blst code, group-checked if gc) and the Jacobian point.
 __global__ __launch_bounds__(WG) void k_parse_sig_list(uint32_t n, const uint8_t* __restrict__ data,
                                                        const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
@@ -909,7 +1014,7 @@ struct ovh_ctx {
   uint32_t* msm_buf[OVH_BATCH_SLOTS] = {};
   uint64_t slot_seed[OVH_BATCH_SLOTS] = {}, slot_base[OVH_BATCH_SLOTS] = {};
   // Fp-VM programs + constant table in device memory
-  VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{};
+  VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{};
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
@@ -948,7 +1053,9 @@ static constexpr size_t LDS_HDBL = ((size_t)SLOT_BASE_W + (64 / VM_HDBL1_W) * (s
 static_assert(VM_MADD_W == VM_PADD_W && VM_HDBL1_W == VM_HDBL2_W && VM_HDBL1_W == VM_HDBL4_W && VM_HDBL1_W == VM_HDBL8_W &&
                   VM_HDBL1_W == VM_HDBL16_W && VM_MADD_NIN == 10 && VM_PADD_NIN == 12 && VM_HDBL1_NIN == 12,
               "MSM program shapes (tools/fpvm/progs.py)");
-static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024, "default LDS limit");
+static constexpr size_t LDS_SIGCHK = ((size_t)SLOT_BASE_W + (64 / VM_SIGCHK_W) * (size_t)SIGCHK_STRIDE_W) * 4;
+static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024 && LDS_SIGCHK <= 64 * 1024,
+              "default LDS limit");
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
 // allocation granules assumed)
@@ -1000,6 +1107,8 @@ static int vm_init(ovh_ctx* c) {
   CHK(vm_upload(c, c->vm_final, VM_FINAL_CODE, VM_FINAL_NPHASES, VM_FINAL_W, VM_FINAL_NW, VM_FINAL_IN, VM_FINAL_NIN, VM_FINAL_OUT,
                 VM_FINAL_NOUT));
   CHK(vm_upload(c, c->vm_rs, VM_RS_CODE, VM_RS_NPHASES, VM_RS_W, VM_RS_NW, VM_RS_IN, VM_RS_NIN, VM_RS_OUT, 0));
+  CHK(vm_upload(c, c->vm_sigchk, VM_SIGCHK_CODE, VM_SIGCHK_NPHASES, VM_SIGCHK_W, VM_SIGCHK_NW, VM_SIGCHK_IN,
+                VM_SIGCHK_NIN, VM_SIGCHK_OUT, VM_SIGCHK_NOUT));
   CHK(vm_upload(c, c->vm_madd, VM_MADD_CODE, VM_MADD_NPHASES, VM_MADD_W, VM_MADD_NW, VM_MADD_IN, VM_MADD_NIN, VM_MADD_OUT,
                 VM_MADD_NOUT));
   CHK(vm_upload(c, c->vm_padd, VM_PADD_CODE, VM_PADD_NPHASES, VM_PADD_W, VM_PADD_NW, VM_PADD_IN, VM_PADD_NIN, VM_PADD_OUT,
@@ -1923,7 +2032,11 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
   c = pick_sub(c);
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  CHK(ensure_scr(c, n > 0 ? n : 1));
+  // compressed signatures go through the VM (k_vm_sigchk + a padd tree, planes [0, 2n) of scr);
+  // lists with other encodings through the one-lane parse and sum
+  bool vm_path = n > 0;
+  for (size_t i = 0; i < n; ++i) vm_path = vm_path && sig_lens[i] == 96;
+  CHK(ensure_scr(c, vm_path ? 2 * n : (n > 0 ? n : 1)));
   CHK(ensure_in(c, list_bytes(sig_lens, n) + list_bytes(pk_lens, n) + 512 + 32 * (n + 1)));
   uint8_t *ds, *dp;
   uint64_t *so, *sl, *po, *pl;
@@ -1933,8 +2046,14 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
   Slab pts{c->scr, c->scr_cap};
   Slab ppts{c->scr + (size_t)6 * 12 * c->scr_cap, c->scr_cap};
   if (n) {
-    k_parse_sig_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, ds, so, sl,
-                                                   (c->flags & OVH_FLAG_AGG_NO_GROUPCHECK) ? 0 : 1, c->scr_sig, pts);
+    const int gc = (c->flags & OVH_FLAG_AGG_NO_GROUPCHECK) ? 0 : 1;
+    if (vm_path) {
+      constexpr uint32_t SL = 64 / VM_SIGCHK_W;
+      k_vm_sigchk<<<(uint32_t)((n + SL - 1) / SL), 64, LDS_SIGCHK, c->stream>>>((uint32_t)n, c->vm_sigchk, c->vm_consts,
+                                                                                ds, so, gc, c->scr_sig, pts);
+    } else {
+      k_parse_sig_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, ds, so, sl, gc, c->scr_sig, pts);
+    }
     k_parse_pk_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, dp, po, pl, c->scr_pk, ppts);
     HIPCHK(hipGetLastError());
   }
@@ -1953,7 +2072,20 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
   if (n == 0) return BLST_AGGR_TYPE_MISMATCH;
   for (size_t i = 0; i < n; ++i)
     if (cs[i] == GROUPCHECK_FAIL) return BLST_POINT_NOT_IN_GROUP;
-  k_sum_g2_compress<<<1, WG, 0, c->stream>>>((uint32_t)n, pts, c->in_buf + used2);
+  if (vm_path) {
+    constexpr uint32_t SL = 64 / VM_PADD_W;
+    uint32_t m = (uint32_t)n, base = 0;
+    while (m > 1) {
+      const uint32_t half = (m + 1) / 2, dst = base ? 0 : (uint32_t)n;
+      k_vm_g2tree<<<(half + SL - 1) / SL, 64, LDS_MSM8, c->stream>>>(m, c->vm_padd, MSM8_STRIDE_W, c->vm_consts,
+                                                                     Slab{pts.p + base, pts.cap}, Slab{pts.p + dst, pts.cap});
+      m = half;
+      base = dst;
+    }
+    k_g2p_compress<<<1, 64, 0, c->stream>>>(Slab{pts.p + base, pts.cap}, c->in_buf + used2);
+  } else {
+    k_sum_g2_compress<<<1, WG, 0, c->stream>>>((uint32_t)n, pts, c->in_buf + used2);
+  }
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out, c->in_buf + used2, 96, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));

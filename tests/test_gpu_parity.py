@@ -324,3 +324,32 @@ def test_shard_verifier_rccl_single_rank(cc):
         assert [i for i in range(n) if c[1, i] != 0] == [9] and c[1, 9] == 5
     finally:
         dist.destroy_process_group()
+
+
+def test_aggregate_vm_tree_matches_oracle(cc, golden):
+    """aggregate_signatures' VM path (k_vm_sigchk + the padd tree) at sizes 1 .. 300, with
+    repeated signatures (the tree doubles), a sigma / -sigma pair, the infinity encoding, and
+    every 96-byte golden signature alone (exact codes and bytes against the C oracle)."""
+    import orc
+    import synth_votes as sv
+    sigs, _, pks = sv.make(cc.ctx, 300, lo=70000)
+    sigs, pks = [bytes(s) for s in sigs], [bytes(p) for p in pks]
+    neg = sv.bls.g2_compress(sv.bls.pt_neg(sv.bls.Fp2Ops, sv.bls.g2_from_bytes(sigs[5])))
+    inf = bytes([0xC0]) + bytes(95)
+    lists = [(sigs[:n], pks[:n]) for n in (1, 2, 3, 67, 128, 129, 300)]
+    lists.append((sigs[:40] + sigs[:40] + [sigs[7]], pks[:40] + pks[:40] + [pks[7]]))
+    lists.append((sigs[:9] + [neg, inf], pks[:11]))
+    for c in golden["verify"]:
+        if len(c["sig"]) == 192:
+            lists.append(([_b(c["sig"])], [pks[0]]))
+            lists.append((sigs[:5] + [_b(c["sig"])], pks[:6]))
+    for ss, ps in lists:
+        want = orc.aggregate_sigs(ss, ps)
+        out = {}
+
+        def run():
+            out["v"] = cc.aggregate_signatures(ss, ps)
+        code = _code(run)
+        assert code == want[0], (len(ss), want)
+        if code == 0:
+            assert out["v"] == want[1], len(ss)

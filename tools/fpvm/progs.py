@@ -12,6 +12,8 @@ layouts. Input and output names are listed in the order the HIP side addresses t
   madd     MSM bucket level 0: B (projective) + A (affine)
   padd     MSM bucket levels >= 1 and the bit-plane sums: A + B (projective)
   hdbl<m>  MSM window combination: A + [2^m] B (projective), m = 1, 2, 4, 8, 16
+  sigchk   aggregate_signatures: one signature's decompression + G2 subgroup check (the vote's
+           "sig" section on its own), affine sigma out for the padd tree that sums them
   fold     4 partials (F_i in Fp12, S_i projective G2) -> (prod F_i, sum S_i)
   final    up to 4 partials -> prod F * Miller(-G1, sum S) -> final exponentiation == 1; also
            the bisection checks of the fallback (one group's partial, or one vote's (f, r sigma):
@@ -194,6 +196,22 @@ def build_hdbl(m):
     return build
 
 
+SIGCHK_IN = ["sig_x0", "sig_x1", "sig_sort"]
+SIGCHK_OUT = ["sig_ok", "sig_grp", "q0", "q1", "q2", "q3"]
+
+
+def build_sigchk():
+    p = Prog("sigchk")
+    a = Alg(p, use_sop=USE_SOP)
+    R = p.const(R_MONT)
+    sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
+    sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
+    sig_grp = a.g2_in_group((qx, qy, (p.one, p.zero)))
+    for name, v in zip(SIGCHK_OUT, [sig_ok, sig_grp, qx[0], qx[1], qy[0], qy[1]]):
+        p.output(name, v)
+    return p
+
+
 FOLD_K = 4
 FOLD_IN = [n for k in range(FOLD_K) for n in f12_names("F%d_" % k) + g2p_names("S%d_" % k)]
 FOLD_OUT = f12_names("F") + g2p_names("S")
@@ -251,3 +269,4 @@ PROGRAMS = {
 }
 for _m in HDBL_M:
     PROGRAMS["hdbl%d" % _m] = (build_hdbl(_m), PA_IN + PB_IN, PT_OUT)
+PROGRAMS["sigchk"] = (build_sigchk, SIGCHK_IN, SIGCHK_OUT)
