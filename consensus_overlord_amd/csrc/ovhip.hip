@@ -701,55 +701,143 @@ __global__ __launch_bounds__(64) void k_gate(const unsigned long long* vstart, u
     __builtin_amdgcn_s_sleep(16);
 }
 
-// Validator table (ovh_set_validators): lane per key, 48-byte compressed -> flags + the point
-// (X : Y : Z) Montgomery, (0 : 1 : 0) for infinity or a failed parse.
-__global__ __launch_bounds__(WG) void k_table_build(uint32_t n, const uint8_t* __restrict__ pks, Slab pts,
-                                                    uint32_t* __restrict__ flags) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  G1A a;
-  bool inf;
-  const int e = g1_from_bytes(a, inf, pks + (size_t)i * 48, 48);
-  uint32_t f = 0;
-  Fp X, Y, Z;
-  fp_zero(X);
-  fp_one(Y);
-  fp_zero(Z);
-  if (e != BLST_SUCCESS) {
-    f = PKF_PARSE;
-  } else if (inf) {
-    f = PKF_INF;
-  } else {
-    X = a.x;
-    Y = a.y;
-    fp_one(Z);
-    G1J j;
-    jac_from_aff(j, a);
-    if (!g1_in_subgroup(j)) f = PKF_GRP;
+// Validator table (ovh_set_validators) and the keys of verify_aggregated_signature: one 48-byte
+// compressed key per 16-lane slice (program "pkchk": decompression + G1 subgroup check) -> flags
+// + the point (X : Y : Z) Montgomery, (0 : 1 : 0) for infinity or a failed parse. Flag precedence
+// as the vote kernel's (k_vm_vote): bad encoding, off the curve or x = 0 -> PKF_PARSE.
+constexpr uint32_t PKCHK_STRIDE_W = align128w(VM_PKCHK_NSLOTS * 12 + 4);
+__global__ __launch_bounds__(64) void k_vm_pkchk(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                 const uint8_t* __restrict__ pks, Slab pts, uint32_t* __restrict__ flags) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / VM_PKCHK_W, lane = threadIdx.x % VM_PKCHK_W;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * PKCHK_STRIDE_W;
+  uint32_t* hdr = slots + VM_PKCHK_NSLOTS * 12;
+  const uint32_t i = blockIdx.x * (64 / VM_PKCHK_W) + slice;
+  const bool active = i < n;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active && lane == 0) {
+    uint32_t x[12], bad, inf, sort, xz;
+    parse_hdr(pks + (size_t)i * 48, 48, x, x, bad, inf, sort, xz);
+    slot_put(slots, VM_PKCHK_IN[VM_PKCHK_IN_PK_X], x);
+    slot_flag(slots, VM_PKCHK_IN[VM_PKCHK_IN_PK_SORT], sort);
+    hdr[0] = bad | inf << 1 | xz << 2;
   }
-  pts.st(X, 0, i);
-  pts.st(Y, 1, i);
-  pts.st(Z, 2, i);
-  flags[i] = f;
+  __syncthreads();
+  vm::run(prog.code, VM_PKCHK_NPHASES, VM_PKCHK_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  __syncthreads();
+  if (!active) return;
+  const uint32_t pf = hdr[0];
+  uint32_t f = 0;
+  if ((pf & 1) || (!(pf & 2) && (!slot_flag_get(slots, VM_PKCHK_OUT[VM_PKCHK_OUT_PK_OK]) || (pf & 4)))) f = PKF_PARSE;
+  else if (pf & 2) f = PKF_INF;
+  else if (!slot_flag_get(slots, VM_PKCHK_OUT[VM_PKCHK_OUT_PK_GRP])) f = PKF_GRP;
+  const bool pt = f == 0 || f == PKF_GRP;
+  for (uint32_t k = lane; k < 3; k += VM_PKCHK_W) {
+    Fp v;
+    if (pt && k < 2) {
+      const uint32_t src = VM_PKCHK_OUT[VM_PKCHK_OUT_P0 + k];
+      for (int l = 0; l < 12; ++l) v.v[l] = slots[src * 12 + l];
+      vm::canon(v, v);
+    } else if (k == (pt ? 2u : 1u)) {
+      fp_one(v);
+    } else {
+      fp_zero(v);
+    }
+    pts.st(v, k, i);
+  }
+  if (lane == 0) flags[i] = f;
 }
 
-// QC batch: lane per QC, apk = sum of the table keys selected by the QC's voter list
-// (sorted-order indices, CSR), homogeneous projective (X Z : Y : Z^3) from Jacobian; flags:
-// PKF_INF when the sum is O.
-__global__ __launch_bounds__(WG) void k_qc_apk(uint32_t nq, const uint32_t* __restrict__ off,
+// One level of an aggregated key's pairwise sum: out[q] = in[2q] + in[2q + 1] (g1padd, complete
+// formulas; the identity past the end), one pair per 8-lane slice.
+__global__ __launch_bounds__(64) void k_vm_g1tree(uint32_t m, VmDev prog, uint32_t stride_w,
+                                                  const uint32_t* __restrict__ cst_g, Slab in, Slab out) {
+  constexpr uint32_t W = VM_G1PADD_W, SL = 64 / W;
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / W, lane = threadIdx.x % W;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * stride_w;
+  const uint32_t q = blockIdx.x * SL + slice;
+  const bool active = q < (m + 1) / 2;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active) {
+    for (uint32_t k = lane; k < 6; k += W) {
+      const uint32_t e = 2 * q + k / 3, c = k % 3;
+      Fp v;
+      if (e < m) in.ld(v, c, e);
+      else if (c == 1) fp_one(v);
+      else fp_zero(v);
+      slot_put(slots, prog.in[k], v.v);
+    }
+  }
+  __syncthreads();
+  vm::run(prog.code, prog.nphases, W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  if (active) {
+    for (uint32_t k = lane; k < 3; k += W) {
+      Fp v;
+      const uint32_t src = prog.out[k];
+      for (int l = 0; l < 12; ++l) v.v[l] = slots[src * 12 + l];
+      vm::canon(v, v);
+      out.st(v, k, q);
+    }
+  }
+}
+
+// element 0 of a tree's last level -> the QC key slot (out element 0), PKF_INF when it is O
+__global__ __launch_bounds__(64) void k_apk_finish(Slab in, Slab out, uint32_t* __restrict__ flags) {
+  const uint32_t k = threadIdx.x;
+  if (k >= 3) return;
+  Fp v;
+  in.ld(v, k, 0);
+  out.st(v, k, 0);
+  if (k == 2) {
+    uint32_t z = 0;
+    for (int l = 0; l < 12; ++l) z |= v.v[l];
+    flags[0] = z ? 0u : PKF_INF;
+  }
+}
+
+// QC batch: one workgroup per QC, apk = sum of the table keys selected by the QC's voter list
+// (sorted-order indices, CSR): each lane sums a strided share (Jacobian), then a 6-level LDS tree;
+// out = homogeneous projective (X Z : Y : Z^3); flags: PKF_INF when the sum is O.
+__global__ __launch_bounds__(64) void k_qc_apk(uint32_t nq, const uint32_t* __restrict__ off,
                                                const uint32_t* __restrict__ ent, Slab table, Slab out,
                                                uint32_t* __restrict__ flags) {
-  const uint32_t q = blockIdx.x * WG + threadIdx.x;
+  __shared__ uint32_t red[64 * 36];
+  const uint32_t q = blockIdx.x, t = threadIdx.x;
   if (q >= nq) return;
   G1J acc, x;
   jac_set_inf(acc);
-  for (uint32_t k = off[q]; k < off[q + 1]; ++k) {
+  for (uint32_t k = off[q] + t; k < off[q + 1]; k += 64) {
     const uint32_t e = ent[k];
     table.ld(x.X, 0, e);
     table.ld(x.Y, 1, e);
     table.ld(x.Z, 2, e);
     jac_add(acc, acc, x);
   }
+  for (uint32_t s = 32; s >= 1; s >>= 1) {
+    if (t >= s && t < 2 * s) {
+      for (int l = 0; l < 12; ++l) {
+        red[(t - s) * 36 + l] = acc.X.v[l];
+        red[(t - s) * 36 + 12 + l] = acc.Y.v[l];
+        red[(t - s) * 36 + 24 + l] = acc.Z.v[l];
+      }
+    }
+    __syncthreads();
+    if (t < s) {
+      for (int l = 0; l < 12; ++l) {
+        x.X.v[l] = red[t * 36 + l];
+        x.Y.v[l] = red[t * 36 + 12 + l];
+        x.Z.v[l] = red[t * 36 + 24 + l];
+      }
+      jac_add(acc, acc, x);
+    }
+    __syncthreads();
+  }
+  if (t) return;
   Fp X, Y, Z;
   uint32_t f = 0;
   if (jac_is_inf(acc)) {
@@ -1014,7 +1102,8 @@ struct ovh_ctx {
   uint32_t* msm_buf[OVH_BATCH_SLOTS] = {};
   uint64_t slot_seed[OVH_BATCH_SLOTS] = {}, slot_base[OVH_BATCH_SLOTS] = {};
   // Fp-VM programs + constant table in device memory
-  VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{};
+  VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{},
+      vm_pkchk{}, vm_g1padd{};
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
@@ -1054,7 +1143,11 @@ static_assert(VM_MADD_W == VM_PADD_W && VM_HDBL1_W == VM_HDBL2_W && VM_HDBL1_W =
                   VM_HDBL1_W == VM_HDBL16_W && VM_MADD_NIN == 10 && VM_PADD_NIN == 12 && VM_HDBL1_NIN == 12,
               "MSM program shapes (tools/fpvm/progs.py)");
 static constexpr size_t LDS_SIGCHK = ((size_t)SLOT_BASE_W + (64 / VM_SIGCHK_W) * (size_t)SIGCHK_STRIDE_W) * 4;
-static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024 && LDS_SIGCHK <= 64 * 1024,
+static constexpr size_t LDS_PKCHK = ((size_t)SLOT_BASE_W + (64 / VM_PKCHK_W) * (size_t)PKCHK_STRIDE_W) * 4;
+static constexpr uint32_t G1PADD_STRIDE_W = align128w(VM_G1PADD_NSLOTS * 12);
+static constexpr size_t LDS_G1PADD = ((size_t)SLOT_BASE_W + (64 / VM_G1PADD_W) * (size_t)G1PADD_STRIDE_W) * 4;
+static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024 && LDS_SIGCHK <= 64 * 1024 &&
+                  LDS_PKCHK <= 64 * 1024 && LDS_G1PADD <= 64 * 1024 && VM_G1PADD_NIN == 6,
               "default LDS limit");
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
@@ -1109,6 +1202,10 @@ static int vm_init(ovh_ctx* c) {
   CHK(vm_upload(c, c->vm_rs, VM_RS_CODE, VM_RS_NPHASES, VM_RS_W, VM_RS_NW, VM_RS_IN, VM_RS_NIN, VM_RS_OUT, 0));
   CHK(vm_upload(c, c->vm_sigchk, VM_SIGCHK_CODE, VM_SIGCHK_NPHASES, VM_SIGCHK_W, VM_SIGCHK_NW, VM_SIGCHK_IN,
                 VM_SIGCHK_NIN, VM_SIGCHK_OUT, VM_SIGCHK_NOUT));
+  CHK(vm_upload(c, c->vm_pkchk, VM_PKCHK_CODE, VM_PKCHK_NPHASES, VM_PKCHK_W, VM_PKCHK_NW, VM_PKCHK_IN, VM_PKCHK_NIN,
+                VM_PKCHK_OUT, VM_PKCHK_NOUT));
+  CHK(vm_upload(c, c->vm_g1padd, VM_G1PADD_CODE, VM_G1PADD_NPHASES, VM_G1PADD_W, VM_G1PADD_NW, VM_G1PADD_IN,
+                VM_G1PADD_NIN, VM_G1PADD_OUT, VM_G1PADD_NOUT));
   CHK(vm_upload(c, c->vm_madd, VM_MADD_CODE, VM_MADD_NPHASES, VM_MADD_W, VM_MADD_NW, VM_MADD_IN, VM_MADD_NIN, VM_MADD_OUT,
                 VM_MADD_NOUT));
   CHK(vm_upload(c, c->vm_padd, VM_PADD_CODE, VM_PADD_NPHASES, VM_PADD_W, VM_PADD_NW, VM_PADD_IN, VM_PADD_NIN, VM_PADD_OUT,
@@ -2146,7 +2243,7 @@ static int ensure_qc_buf(ovh_ctx* c, size_t nd) {
 }
 
 // verify_aggregated_signature (consensus.rs:365-382) on the batch kernels: the keys decoded and
-// group-checked lane by lane (k_table_build), their sum (k_qc_apk), then the vote_t program and
+// group-checked on the VM (k_vm_pkchk), their sum (a g1padd tree), then the vote_t program and
 // the final check for the one (sig, hash, apk). Returns 1 when the exact one-lane path must
 // decide instead (a key outside G1: the sum's own group check decides; other encodings).
 static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, const uint8_t* hash,
@@ -2154,31 +2251,26 @@ static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_l
   if (n == 0 || agg_len != 96 || !hash || hash_len != 32) return 1;
   for (size_t i = 0; i < n; ++i)
     if (pk_lens[i] != 48) return 1;
-  if (n > c->qt_cap || !c->qt_buf) {
+  if (2 * n > c->qt_cap || !c->qt_buf) {  // keys in [0, n), the tree's levels ping-pong over [0, 2n)
     if (c->qt_buf) (void)hipFree(c->qt_buf);
     c->qt_buf = nullptr;
     c->qt_cap = 0;
     uint32_t cap = 64;
-    while (cap < n) cap <<= 1;
+    while (cap < 2 * n) cap <<= 1;
     HIPCHK(hipMalloc(&c->qt_buf, (size_t)(3 * 12 + 1) * cap * 4));
     c->qt_cap = cap;
   }
   CHK(ensure_qc_buf(c, 1));
-  CHK(ensure_in(c, n * 48 + 96 + 32 + 64 + 8 * (n + 1)));
-  uint8_t* d = c->in_buf;  // keys | sig | hash | code | off[2] | ent[n]
+  CHK(ensure_in(c, n * 48 + 96 + 32 + 64));
+  uint8_t* d = c->in_buf;  // keys | sig | hash | code
   int32_t* dc = (int32_t*)(d + ((n * 48 + 128 + 15) & ~(size_t)15));
-  uint32_t* doff = (uint32_t*)(dc + 4);
-  uint32_t* dent = doff + 2;
-  std::vector<uint32_t> hv(2 + n);
-  hv[0] = 0;
-  hv[1] = (uint32_t)n;
-  for (size_t i = 0; i < n; ++i) hv[2 + i] = (uint32_t)i;
   HIPCHK(hipMemcpyAsync(d, pks, n * 48, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(d + n * 48, agg_sig, 96, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(d + n * 48 + 96, hash, 32, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(doff, hv.data(), hv.size() * 4, hipMemcpyHostToDevice, c->stream));
   uint32_t* kflags = c->qt_buf + (size_t)3 * 12 * c->qt_cap;
-  k_table_build<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, d, Slab{c->qt_buf, c->qt_cap}, kflags);
+  constexpr uint32_t PK_SL = 64 / VM_PKCHK_W;
+  k_vm_pkchk<<<(uint32_t)((n + PK_SL - 1) / PK_SL), 64, LDS_PKCHK, c->stream>>>((uint32_t)n, c->vm_pkchk, c->vm_consts, d,
+                                                                               Slab{c->qt_buf, c->qt_cap}, kflags);
   HIPCHK(hipGetLastError());
   std::vector<uint32_t> hf(n);
   HIPCHK(hipMemcpyAsync(hf.data(), kflags, n * 4, hipMemcpyDeviceToHost, c->stream));
@@ -2192,7 +2284,19 @@ static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_l
   }
   if (fl & PKF_GRP) return 1;
   uint32_t* qflags = c->qc_buf + (size_t)3 * 12 * c->qc_cap;
-  k_qc_apk<<<1, WG, 0, c->stream>>>(1, doff, dent, Slab{c->qt_buf, c->qt_cap}, Slab{c->qc_buf, c->qc_cap}, qflags);
+  {
+    constexpr uint32_t SL = 64 / VM_G1PADD_W;
+    uint32_t m = (uint32_t)n, base = 0;
+    while (m > 1) {
+      const uint32_t half = (m + 1) / 2, dst = base ? 0 : (uint32_t)n;
+      k_vm_g1tree<<<(half + SL - 1) / SL, 64, LDS_G1PADD, c->stream>>>(m, c->vm_g1padd, G1PADD_STRIDE_W, c->vm_consts,
+                                                                       Slab{c->qt_buf + base, c->qt_cap},
+                                                                       Slab{c->qt_buf + dst, c->qt_cap});
+      m = half;
+      base = dst;
+    }
+    k_apk_finish<<<1, 64, 0, c->stream>>>(Slab{c->qt_buf + base, c->qt_cap}, Slab{c->qc_buf, c->qc_cap}, qflags);
+  }
   HIPCHK(hipGetLastError());
   CHK(ensure_cap(c, 1));
   CHK(verify_async_locked(c, 1, d + n * 48, d + n * 48 + 96, KeySrc{nullptr, PkSrc{c->qc_buf, c->qc_cap, qflags, nullptr}},
@@ -2265,7 +2369,9 @@ static int set_validators_locked(ovh_ctx* c, const uint8_t* pks, size_t n) {
   if (n) {
     CHK(ensure_in(c, n * 48 + 64));
     HIPCHK(hipMemcpyAsync(c->in_buf, pks, n * 48, hipMemcpyHostToDevice, c->stream));
-    k_table_build<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, c->in_buf, Slab{t.planes, t.cap}, t.flags);
+    constexpr uint32_t PK_SL = 64 / VM_PKCHK_W;
+    k_vm_pkchk<<<(uint32_t)((n + PK_SL - 1) / PK_SL), 64, LDS_PKCHK, c->stream>>>((uint32_t)n, c->vm_pkchk, c->vm_consts,
+                                                                                 c->in_buf, Slab{t.planes, t.cap}, t.flags);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(t.hflags.data(), t.flags, n * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -2400,7 +2506,7 @@ static int qc_batch_locked(ovh_ctx* c, size_t nq, const uint8_t* sigs, const uin
   HIPCHK(hipMemcpyAsync(doff, off.data(), off.size() * 4, hipMemcpyHostToDevice, c->stream));
   if (!ent.empty()) HIPCHK(hipMemcpyAsync(dent, ent.data(), ent.size() * 4, hipMemcpyHostToDevice, c->stream));
   uint32_t* qflags = c->qc_buf + (size_t)3 * 12 * c->qc_cap;
-  k_qc_apk<<<nblk(nd), WG, 0, c->stream>>>((uint32_t)nd, doff, dent, Slab{t.planes, t.cap},
+  k_qc_apk<<<(uint32_t)nd, 64, 0, c->stream>>>((uint32_t)nd, doff, dent, Slab{t.planes, t.cap},
                                           Slab{c->qc_buf, c->qc_cap}, qflags);
   HIPCHK(hipGetLastError());
   CHK(verify_async_locked(c, nd, d, d + nd * 96, KeySrc{nullptr, PkSrc{c->qc_buf, c->qc_cap, qflags, nullptr}}, dc));

@@ -14,6 +14,9 @@ layouts. Input and output names are listed in the order the HIP side addresses t
   hdbl<m>  MSM window combination: A + [2^m] B (projective), m = 1, 2, 4, 8, 16
   sigchk   aggregate_signatures: one signature's decompression + G2 subgroup check (the vote's
            "sig" section on its own), affine sigma out for the padd tree that sums them
+  pkchk    a public key's decompression + G1 subgroup check (the validator table and the keys of
+           verify_aggregated_signature), affine key out
+  g1padd   A + B in G1 (projective): the pairwise tree that sums an aggregated key
   fold     4 partials (F_i in Fp12, S_i projective G2) -> (prod F_i, sum S_i)
   final    up to 4 partials -> prod F * Miller(-G1, sum S) -> final exponentiation == 1; also
            the bisection checks of the fallback (one group's partial, or one vote's (f, r sigma):
@@ -212,6 +215,35 @@ def build_sigchk():
     return p
 
 
+PKCHK_IN = ["pk_x", "pk_sort"]
+PKCHK_OUT = ["pk_ok", "pk_grp", "p0", "p1"]
+
+
+def build_pkchk():
+    p = Prog("pkchk")
+    a = Alg(p, use_sop=USE_SOP)
+    R = p.const(R_MONT)
+    pk_ok, (px, py) = a.g1_decompress(p.input("pk_x") * R, p.input("pk_sort"))
+    pk_grp, _ = a.g1_in_group((px, py, p.one))
+    for name, v in zip(PKCHK_OUT, [pk_ok, pk_grp, px, py]):
+        p.output(name, v)
+    return p
+
+
+G1A_IN = ["a%d" % k for k in range(3)]
+G1B_IN = ["b%d" % k for k in range(3)]
+G1_OUT = ["s%d" % k for k in range(3)]
+
+
+def build_g1padd():
+    p = Prog("g1padd")
+    a = Alg(p, use_sop=USE_SOP)
+    S = a.pt_add("fp", tuple(p.input(n) for n in G1A_IN), tuple(p.input(n) for n in G1B_IN))
+    for name, v in zip(G1_OUT, S):
+        p.output(name, v)
+    return p
+
+
 FOLD_K = 4
 FOLD_IN = [n for k in range(FOLD_K) for n in f12_names("F%d_" % k) + g2p_names("S%d_" % k)]
 FOLD_OUT = f12_names("F") + g2p_names("S")
@@ -270,3 +302,5 @@ PROGRAMS = {
 for _m in HDBL_M:
     PROGRAMS["hdbl%d" % _m] = (build_hdbl(_m), PA_IN + PB_IN, PT_OUT)
 PROGRAMS["sigchk"] = (build_sigchk, SIGCHK_IN, SIGCHK_OUT)
+PROGRAMS["pkchk"] = (build_pkchk, PKCHK_IN, PKCHK_OUT)
+PROGRAMS["g1padd"] = (build_g1padd, G1A_IN + G1B_IN, G1_OUT)
