@@ -1054,6 +1054,7 @@ struct ovh_ctx {
   // Batches alternate between two final streams, so two finals may run at once (each shares a
   // SIMD with a vote wave and takes longer than a vote kernel there).
   hipStream_t fstream = nullptr, fstream2 = nullptr;
+  hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse)
   hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
@@ -1817,6 +1818,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->part_out, 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
             hipMalloc(&c->vstart, 8) == hipSuccess && hipMemset(c->vstart, 0, 8) == hipSuccess &&
             hipMemset(c->result, 0, 64) == hipSuccess &&
@@ -1872,7 +1874,7 @@ ovh_ctx* ovh_create_multi(const int* devices, int ndev, const uint8_t* dst, size
 static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k]})
@@ -1893,7 +1895,7 @@ static void destroy_one(ovh_ctx* c) {
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream})
     if (s) (void)hipStreamDestroy(s);
   delete c;
 }
@@ -2143,6 +2145,12 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
   Slab pts{c->scr, c->scr_cap};
   Slab ppts{c->scr + (size_t)6 * 12 * c->scr_cap, c->scr_cap};
   if (n) {
+    // the keys parse on the side stream while the signatures run through the VM
+    HIPCHK(hipEventRecord(c->ev_x[2], c->stream));  // staged inputs
+    HIPCHK(hipStreamWaitEvent(c->xstream, c->ev_x[2], 0));
+    k_parse_pk_list<<<nblk(n), WG, 0, c->xstream>>>((uint32_t)n, dp, po, pl, c->scr_pk, ppts);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev_x[3], c->xstream));
     const int gc = (c->flags & OVH_FLAG_AGG_NO_GROUPCHECK) ? 0 : 1;
     if (vm_path) {
       constexpr uint32_t SL = 64 / VM_SIGCHK_W;
@@ -2151,8 +2159,8 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
     } else {
       k_parse_sig_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, ds, so, sl, gc, c->scr_sig, pts);
     }
-    k_parse_pk_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, dp, po, pl, c->scr_pk, ppts);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamWaitEvent(c->stream, c->ev_x[3], 0));
   }
   std::vector<int32_t> cs(n), cp(n);
   if (n) {
