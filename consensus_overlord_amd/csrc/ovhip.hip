@@ -1523,6 +1523,10 @@ static int enqueue_msm(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, const i
 // Bisection of the batch in `slot` on stream `st`, skipped on the device when *d_verdict == 1
 // (d_verdict null: always runs): the 16-vote groups' own checks (R1 partials), then per-vote
 // checks of the votes in failing groups.
+// up to one vote per SIMD (256 CUs x 4): the per-vote checks of a whole batch run side by side
+#ifndef BISECT_DIRECT_MAX
+#define BISECT_DIRECT_MAX 1024u
+#endif
 static void enqueue_bisect(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, int32_t* d_codes,
                            const int32_t* d_verdict) {
   StageScope p(c, ST_FALLBACK, st);
@@ -1531,6 +1535,14 @@ static void enqueue_bisect(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, int
   Slab s{c->state_slot[slot], c->cap};
   k_vm_rs<<<(n + 64 / VM_RS_W - 1) / (64 / VM_RS_W), 64, LDS_RS, st>>>(n, c->vm_rs, c->vm_consts, s, c->slot_seed[slot],
                                                                      c->slot_base[slot], d_codes, d_verdict);
+  if (n <= BISECT_DIRECT_MAX) {
+    // small batches: every vote with code 0 straight through the per-vote check (one level of
+    // final-program latency instead of the group level and then the vote level)
+    (void)hipMemsetAsync(c->grp_ok[slot], 0, (size_t)g * 4, st);
+    k_vm_votechk<<<n, 64, LDS_FINAL, st>>>(n, c->vm_final, c->vm_consts, Slab{c->state_slot[slot], c->cap}, d_codes,
+                                           d_verdict, c->grp_ok[slot]);
+    return;
+  }
   const uint32_t nwg = (n + 3) / 4;
   k_vm_fold<VM_FOLD_UNITS><<<(nwg + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(
       n, c->vm_fold, c->vm_consts, Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{s.p + (size_t)S_RS * 12 * s.cap, s.cap},
