@@ -121,6 +121,8 @@ def latencies(ctx, sigs, hs, pks) -> dict:
     """Untimed latency probes after the throughput run (configs 2 and 5 report
     latency; the reference's own call shape is one verify_signature per vote):
       verify_ms      one ovh_verify (Crypto::verify_signature) of a valid vote, median of 5
+      sign_ms        one ovh_sign (Crypto::sign) of a vote digest, median of 3
+      aggregate67_ms config 2: aggregate_signatures over 67 signatures, median of 3
       qc67_ms        config 2: verify_aggregated_signature over 67 voters, median of 3
       qc_table_ms    config 2 through the validator table (ovh_verify_qc_batch, one QC)
       cfg5_ms        config 5: 1024 votes with 1% sigma + G2, batch incl. bisection, median of 3
@@ -140,6 +142,9 @@ def latencies(ctx, sigs, hs, pks) -> dict:
         return round(float(np.median(ts)) * 1e3, 3)
     assert lib.ovh_verify(ctx.ptr, s0, 96, h0, 32, p0, 48) == 0
     out["verify_ms"] = med(lambda: lib.ovh_verify(ctx.ptr, s0, 96, h0, 32, p0, 48), 5)
+    sk0, sgo = bytes(31) + b"\x05", ctypes.create_string_buffer(96)
+    assert lib.ovh_sign(ctx.ptr, sk0, 32, h0, 32, sgo) == 0
+    out["sign_ms"] = med(lambda: lib.ovh_sign(ctx.ptr, sk0, 32, h0, 32, sgo), 3)
     # config 2: 67 of 100 validators sign one vote digest; aggregate made with the library
     n = 67
     digest = h0

@@ -686,6 +686,84 @@ __global__ __launch_bounds__(64) void k_g2p_compress(Slab in, uint8_t* out) {
   g2_compress(out, j);
 }
 
+// Crypto::sign (consensus.rs:390-395) on the VM: one signature per 16-lane slice. sign0 hashes
+// to G2 (u0, u1 from k_h2f) and multiplies by the top 64 bits of the secret scalar, sign1 runs
+// three times for the rest: the scalar enters only as the selb bits of each launch, so the
+// instruction stream does not depend on it. Lane 0 of the slice compresses the result.
+constexpr uint32_t SIGN_NSLOTS = VM_SIGN0_NSLOTS > VM_SIGN1_NSLOTS ? VM_SIGN0_NSLOTS : VM_SIGN1_NSLOTS;
+constexpr uint32_t SIGN_STRIDE_W = align128w(SIGN_NSLOTS * 12 + 6 * 12);  // + H stash
+__global__ __launch_bounds__(64) void k_vm_sign(uint32_t n, VmDev p0, VmDev p1, const uint32_t* __restrict__ cst_g,
+                                                const uint8_t* __restrict__ sks, Slab s, uint8_t* __restrict__ out) {
+  static_assert(VM_SIGN0_W == VM_SIGN1_W && VM_SIGN0_NOUT == 12 && VM_SIGN1_NIN == 12 && VM_SIGN1_NOUT == 6,
+                "sign program shapes (tools/fpvm/progs.py)");
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / VM_SIGN0_W, lane = threadIdx.x % VM_SIGN0_W;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * SIGN_STRIDE_W;
+  uint32_t* hst = slots + SIGN_NSLOTS * 12;
+  const uint32_t i = blockIdx.x * (64 / VM_SIGN0_W) + slice;
+  const bool active = i < n;
+  load_consts(cst, cst_g, VM_NCONST);
+  uint64_t k[4] = {0, 0, 0, 0};  // big-endian 64-bit chunks, k[0] the most significant
+  if (active) {
+    const uint8_t* b = sks + (size_t)i * 32;
+    for (int j = 0; j < 4; ++j)
+      for (int t = 0; t < 8; ++t) k[j] = k[j] << 8 | b[8 * j + t];
+    if (lane < 4) {
+      Fp u;
+      s.ld(u, S_U + lane, i);
+      slot_put(slots, VM_SIGN0_IN[lane], u.v);
+    }
+  }
+  __syncthreads();
+  vm::run(p0.code, VM_SIGN0_NPHASES, VM_SIGN0_W, lane, active, slots, cst, k[0], vm::Out{nullptr, 0, 0});
+  __syncthreads();
+  uint32_t v[12];
+  if (active && lane < 12) {
+    const uint32_t src = VM_SIGN0_OUT[lane];
+    for (int l = 0; l < 12; ++l) v[l] = slots[src * 12 + l];
+    if (lane >= 6)
+      for (int l = 0; l < 12; ++l) hst[(lane - 6) * 12 + l] = v[l];
+  }
+  __syncthreads();
+  for (int r = 1; r < 4; ++r) {
+    if (active && lane < 12) slot_put(slots, VM_SIGN1_IN[lane], lane < 6 ? v : hst + (lane - 6) * 12);
+    __syncthreads();
+    vm::run(p1.code, VM_SIGN1_NPHASES, VM_SIGN1_W, lane, active, slots, cst, k[r], vm::Out{nullptr, 0, 0});
+    __syncthreads();
+    if (active && lane < 6) {
+      const uint32_t src = VM_SIGN1_OUT[lane];
+      for (int l = 0; l < 12; ++l) v[l] = slots[src * 12 + l];
+    }
+    __syncthreads();
+  }
+  if (active && lane < 6) {
+    Fp t;
+    for (int l = 0; l < 12; ++l) t.v[l] = v[l];
+    vm::canon(t, t);
+    for (int l = 0; l < 12; ++l) hst[lane * 12 + l] = t.v[l];
+  }
+  __syncthreads();
+  if (active && lane == 0) {
+    Fp2 X, Y, Z, zz;
+    for (int l = 0; l < 12; ++l) {
+      X.c0.v[l] = hst[l];
+      X.c1.v[l] = hst[12 + l];
+      Y.c0.v[l] = hst[24 + l];
+      Y.c1.v[l] = hst[36 + l];
+      Z.c0.v[l] = hst[48 + l];
+      Z.c1.v[l] = hst[60 + l];
+    }
+    G2J j;
+    fp2_mul(j.X, X, Z);
+    fp2_sqr(zz, Z);
+    fp2_mul(j.Y, Y, zz);
+    j.Z = Z;
+    g2_compress(out + (size_t)i * 96, j);
+  }
+}
+
 #include "msm.hpp"
 
 #define GATE_TICKS 30000ull  // 300 us of the 100 MHz wall clock
@@ -996,20 +1074,6 @@ __device__ void sk_words(uint32_t k[8], const uint8_t* sk) {
   }
 }
 
-__global__ __launch_bounds__(WG) void k_sign(uint32_t n, const uint8_t* __restrict__ sks,
-                                             const uint8_t* __restrict__ hashes, XmdTemplates t,
-                                             uint8_t* __restrict__ sigs) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  uint32_t k[8], msg[8];
-  sk_words(k, sks + (size_t)i * 32);
-  be_words_from_bytes(msg, hashes + (size_t)i * 32, 8);
-  G2J h, s;
-  hash_to_g2(h, msg, t);
-  jac_mul_words(s, h, k, 8);
-  g2_compress(sigs + (size_t)i * 96, s);
-}
-
 __global__ __launch_bounds__(WG) void k_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sks, uint8_t* __restrict__ pks) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n) return;
@@ -1104,7 +1168,7 @@ struct ovh_ctx {
   uint64_t slot_seed[OVH_BATCH_SLOTS] = {}, slot_base[OVH_BATCH_SLOTS] = {};
   // Fp-VM programs + constant table in device memory
   VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{},
-      vm_pkchk{}, vm_g1padd{};
+      vm_pkchk{}, vm_g1padd{}, vm_sign0{}, vm_sign1{};
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
@@ -1144,11 +1208,12 @@ static_assert(VM_MADD_W == VM_PADD_W && VM_HDBL1_W == VM_HDBL2_W && VM_HDBL1_W =
                   VM_HDBL1_W == VM_HDBL16_W && VM_MADD_NIN == 10 && VM_PADD_NIN == 12 && VM_HDBL1_NIN == 12,
               "MSM program shapes (tools/fpvm/progs.py)");
 static constexpr size_t LDS_SIGCHK = ((size_t)SLOT_BASE_W + (64 / VM_SIGCHK_W) * (size_t)SIGCHK_STRIDE_W) * 4;
+static constexpr size_t LDS_SIGN = ((size_t)SLOT_BASE_W + (64 / VM_SIGN0_W) * (size_t)SIGN_STRIDE_W) * 4;
 static constexpr size_t LDS_PKCHK = ((size_t)SLOT_BASE_W + (64 / VM_PKCHK_W) * (size_t)PKCHK_STRIDE_W) * 4;
 static constexpr uint32_t G1PADD_STRIDE_W = align128w(VM_G1PADD_NSLOTS * 12);
 static constexpr size_t LDS_G1PADD = ((size_t)SLOT_BASE_W + (64 / VM_G1PADD_W) * (size_t)G1PADD_STRIDE_W) * 4;
 static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024 && LDS_SIGCHK <= 64 * 1024 &&
-                  LDS_PKCHK <= 64 * 1024 && LDS_G1PADD <= 64 * 1024 && VM_G1PADD_NIN == 6,
+                  LDS_PKCHK <= 64 * 1024 && LDS_G1PADD <= 64 * 1024 && LDS_SIGN <= 64 * 1024 && VM_G1PADD_NIN == 6,
               "default LDS limit");
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
@@ -1205,6 +1270,10 @@ static int vm_init(ovh_ctx* c) {
                 VM_SIGCHK_NIN, VM_SIGCHK_OUT, VM_SIGCHK_NOUT));
   CHK(vm_upload(c, c->vm_pkchk, VM_PKCHK_CODE, VM_PKCHK_NPHASES, VM_PKCHK_W, VM_PKCHK_NW, VM_PKCHK_IN, VM_PKCHK_NIN,
                 VM_PKCHK_OUT, VM_PKCHK_NOUT));
+  CHK(vm_upload(c, c->vm_sign0, VM_SIGN0_CODE, VM_SIGN0_NPHASES, VM_SIGN0_W, VM_SIGN0_NW, VM_SIGN0_IN, VM_SIGN0_NIN,
+                VM_SIGN0_OUT, VM_SIGN0_NOUT));
+  CHK(vm_upload(c, c->vm_sign1, VM_SIGN1_CODE, VM_SIGN1_NPHASES, VM_SIGN1_W, VM_SIGN1_NW, VM_SIGN1_IN, VM_SIGN1_NIN,
+                VM_SIGN1_OUT, VM_SIGN1_NOUT));
   CHK(vm_upload(c, c->vm_g1padd, VM_G1PADD_CODE, VM_G1PADD_NPHASES, VM_G1PADD_W, VM_G1PADD_NW, VM_G1PADD_IN,
                 VM_G1PADD_NIN, VM_G1PADD_OUT, VM_G1PADD_NOUT));
   CHK(vm_upload(c, c->vm_madd, VM_MADD_CODE, VM_MADD_NPHASES, VM_MADD_W, VM_MADD_NW, VM_MADD_IN, VM_MADD_NIN, VM_MADD_OUT,
@@ -2017,6 +2086,18 @@ int ovh_sk_parse(ovh_ctx* c, const uint8_t* key, size_t key_len, uint8_t out_sca
   return sk_parse(c, key, key_len, out_scalar);
 }
 
+// n signatures on c->stream: hash_to_field per hash (k_h2f, u planes in scr), then the VM
+// (k_vm_sign). Caller holds c->mu and has sized scr for n.
+static int enqueue_sign(ovh_ctx* c, size_t n, const uint8_t* d_sks, const uint8_t* d_hashes, uint8_t* d_sigs) {
+  Slab u{c->scr, c->scr_cap};
+  k_h2f<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, d_hashes, c->xmd, u);
+  constexpr uint32_t SL = 64 / VM_SIGN0_W;
+  k_vm_sign<<<(uint32_t)((n + SL - 1) / SL), 64, LDS_SIGN, c->stream>>>((uint32_t)n, c->vm_sign0, c->vm_sign1, c->vm_consts,
+                                                                        d_sks, u, d_sigs);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int ovh_sign(ovh_ctx* c, const uint8_t* key, size_t key_len, const uint8_t* hash, size_t hash_len, uint8_t out[96]) {
   if (!c || !out) return OVH_ERR_ARG;
   if (hash_len != 32 || !hash) return OVH_ERR_HASH_LEN;
@@ -2026,10 +2107,10 @@ int ovh_sign(ovh_ctx* c, const uint8_t* key, size_t key_len, const uint8_t* hash
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   CHK(ensure_in(c, 256));
+  CHK(ensure_scr(c, 1));
   HIPCHK(hipMemcpyAsync(c->in_buf, sk, 32, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->in_buf + 32, hash, 32, hipMemcpyHostToDevice, c->stream));
-  k_sign<<<1, WG, 0, c->stream>>>(1, c->in_buf, c->in_buf + 32, c->xmd, c->in_buf + 64);
-  HIPCHK(hipGetLastError());
+  CHK(enqueue_sign(c, 1, c->in_buf, c->in_buf + 32, c->in_buf + 64));
   HIPCHK(hipMemcpyAsync(out, c->in_buf + 64, 96, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
@@ -2743,8 +2824,8 @@ int ovh_sign_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sks, const uint
   if (n == 0) return 0;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  k_sign<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, d_sks, d_hashes, c->xmd, d_sigs);
-  HIPCHK(hipGetLastError());
+  CHK(ensure_scr(c, n));
+  CHK(enqueue_sign(c, n, d_sks, d_hashes, d_sigs));
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
 }

@@ -353,3 +353,30 @@ def test_aggregate_vm_tree_matches_oracle(cc, golden):
         assert code == want[0], (len(ss), want)
         if code == 0:
             assert out["v"] == want[1], len(ss)
+
+
+def test_vm_sign_edge_scalars(cc):
+    """Crypto::sign on the VM (sign0 + 3 x sign1, the scalar as selb bits of four 64-bit
+    launches): scalars with empty 64-bit chunks, single bits, r - 1 and random ones, batch and
+    per-call, against the C oracle."""
+    import torch
+    import orc
+    from consensus_overlord_amd import device as dev
+    r = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    rng = random.Random(0x516)
+    ks = [1, 2, 3, 2 ** 64 - 1, 2 ** 64, 2 ** 128 + 1, 2 ** 192, 2 ** 254, r - 1, r - 2 ** 64]
+    ks += [rng.randrange(1, r) for _ in range(54)]
+    sks = [k.to_bytes(32, "big") for k in ks]
+    hs = [hashlib.sha256(b"sign %d" % i).digest() for i in range(len(ks))]
+    want = [orc.sign(sk, h) for sk, h in zip(sks, hs)]
+    assert all(w[0] == 0 for w in want)
+    d_sk = torch.from_numpy(np.frombuffer(b"".join(sks), dtype=np.uint8).reshape(-1, 32).copy()).cuda()
+    d_h = torch.from_numpy(np.frombuffer(b"".join(hs), dtype=np.uint8).reshape(-1, 32).copy()).cuda()
+    got = dev.sign_batch(cc.ctx, d_sk, d_h).cpu().numpy()
+    for i, w in enumerate(want):
+        assert bytes(got[i]) == w[1], ks[i]
+    from consensus_overlord_amd.crypto import FLAG_SK_RAW, Context
+    import consensus_overlord_amd as coa
+    ctx = Context(flags=FLAG_SK_RAW)
+    for i in (0, 4, 8, 9, 20):
+        assert coa.ConsensusCrypto(sks[i], ctx=ctx).sign(hs[i]) == want[i][1], ks[i]

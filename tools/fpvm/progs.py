@@ -17,6 +17,9 @@ layouts. Input and output names are listed in the order the HIP side addresses t
   pkchk    a public key's decompression + G1 subgroup check (the validator table and the keys of
            verify_aggregated_signature), affine key out
   g1padd   A + B in G1 (projective): the pairwise tree that sums an aggregated key
+  sign0    Crypto::sign, first part: H = hash_to_G2(u0, u1), then [k]H for the top 64 bits k of
+           the secret scalar (selb on the launch's scalar: the schedule does not depend on it)
+  sign1    acc -> [2^64] acc + [k] H for the next 64 bits (run three times)
   fold     4 partials (F_i in Fp12, S_i projective G2) -> (prod F_i, sum S_i)
   final    up to 4 partials -> prod F * Miller(-G1, sum S) -> final exponentiation == 1; also
            the bisection checks of the fallback (one group's partial, or one vote's (f, r sigma):
@@ -244,6 +247,44 @@ def build_g1padd():
     return p
 
 
+def _smul64(a, acc, H, first=False):
+    """MSB-first double-and-add over the launch scalar's 64 bits (complete formulas, selb)."""
+    start = 63
+    if first:   # acc = O: the top bit only selects
+        acc = a.pt_selb("f2", 63, acc, H)
+        start = 62
+    for b in range(start, -1, -1):
+        acc = a.pt_dbl("f2", acc)
+        acc = a.pt_selb("f2", b, acc, a.pt_add("f2", acc, H))
+    return acc
+
+
+SIGN0_IN = ["u00", "u01", "u10", "u11"]
+SIGN_ACC = ["c%d" % k for k in range(6)]
+SIGN_H = ["h%d" % k for k in range(6)]
+
+
+def build_sign0():
+    p = Prog("sign0")
+    a = Alg(p, use_sop=USE_SOP)
+    H = a.hash_to_g2((p.input("u00"), p.input("u01")), (p.input("u10"), p.input("u11")))
+    O = ((p.zero, p.zero), (p.one, p.zero), (p.zero, p.zero))
+    acc = _smul64(a, O, H, first=True)
+    for name, v in zip(SIGN_ACC + SIGN_H, flat_g2p(acc) + flat_g2p(H)):
+        p.output(name, v)
+    return p
+
+
+def build_sign1():
+    p = Prog("sign1")
+    a = Alg(p, use_sop=USE_SOP)
+    acc = _pt_in(p, SIGN_ACC)
+    H = _pt_in(p, SIGN_H)
+    for name, v in zip(SIGN_ACC, flat_g2p(_smul64(a, acc, H))):
+        p.output(name, v)
+    return p
+
+
 FOLD_K = 4
 FOLD_IN = [n for k in range(FOLD_K) for n in f12_names("F%d_" % k) + g2p_names("S%d_" % k)]
 FOLD_OUT = f12_names("F") + g2p_names("S")
@@ -303,4 +344,6 @@ for _m in HDBL_M:
     PROGRAMS["hdbl%d" % _m] = (build_hdbl(_m), PA_IN + PB_IN, PT_OUT)
 PROGRAMS["sigchk"] = (build_sigchk, SIGCHK_IN, SIGCHK_OUT)
 PROGRAMS["pkchk"] = (build_pkchk, PKCHK_IN, PKCHK_OUT)
+PROGRAMS["sign0"] = (build_sign0, SIGN0_IN, SIGN_ACC + SIGN_H)
+PROGRAMS["sign1"] = (build_sign1, SIGN_ACC + SIGN_H, SIGN_ACC)
 PROGRAMS["g1padd"] = (build_g1padd, G1A_IN + G1B_IN, G1_OUT)
