@@ -499,6 +499,123 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
             Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{nullptr, 0}, part0, codes);
 }
 
+// One standalone vote (ovh_verify, verify_aggregated_signature: a batch of one needs no RLC
+// coefficient): programs vote1 / vote_t1 on a whole 64-lane wave compute
+// f = Miller(pk, H) Miller(-G1, sigma) as one two-pair Miller loop, stored to the F planes of
+// element 0, and the code (precedence as k_vm_vote / k_vm_vote_t); k_vm_final1 then checks
+// FE(f) == 1. No MSM, no fold, no bisection: the vote's own pairing equation is the check.
+template <bool TABLE>
+__global__ __launch_bounds__(64) void k_vm_vote1(VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                 const uint8_t* __restrict__ pk_bytes, PkSrc pk,
+                                                 const uint8_t* __restrict__ sig, Slab s, int32_t* __restrict__ code) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  uint32_t* slots = lds + SLOT_BASE_W;
+  constexpr uint32_t NS = TABLE ? VM_VOTE_T1_NSLOTS : VM_VOTE1_NSLOTS;
+  constexpr uint32_t NPH = TABLE ? VM_VOTE_T1_NPHASES : VM_VOTE1_NPHASES;
+  static_assert(VM_VOTE1_W == 64 && VM_VOTE_T1_W == 64, "standalone vote programs take a whole wave");
+  uint32_t* hdr = slots + NS * 12;  // [sig flags, pk flags]
+  const uint32_t lane = threadIdx.x;
+  load_consts(cst, cst_g, VM_NCONST);
+  const uint32_t e = TABLE && pk.idx ? (uint32_t)pk.idx[0] : 0u;
+  if (lane == 0) {
+    uint32_t x1[12], x0[12], bad, inf, sort, xz;
+    parse_hdr(sig, 96, x1, x0, bad, inf, sort, xz);
+    if constexpr (TABLE) {
+      slot_put(slots, VM_VOTE_T1_IN[VM_VOTE_T1_IN_SIG_X1], x1);
+      slot_put(slots, VM_VOTE_T1_IN[VM_VOTE_T1_IN_SIG_X0], x0);
+      slot_flag(slots, VM_VOTE_T1_IN[VM_VOTE_T1_IN_SIG_SORT], sort);
+    } else {
+      slot_put(slots, VM_VOTE1_IN[VM_VOTE1_IN_SIG_X1], x1);
+      slot_put(slots, VM_VOTE1_IN[VM_VOTE1_IN_SIG_X0], x0);
+      slot_flag(slots, VM_VOTE1_IN[VM_VOTE1_IN_SIG_SORT], sort);
+    }
+    hdr[0] = bad | inf << 1 | xz << 2;
+  } else if (lane == 1) {
+    if constexpr (TABLE) {
+      hdr[1] = pk.flags[e];
+    } else {
+      uint32_t x[12], bad, inf, sort, xz;
+      parse_hdr(pk_bytes, 48, x, x, bad, inf, sort, xz);
+      slot_put(slots, VM_VOTE1_IN[VM_VOTE1_IN_PK_X], x);
+      slot_flag(slots, VM_VOTE1_IN[VM_VOTE1_IN_PK_SORT], sort);
+      hdr[1] = bad | inf << 1 | xz << 2;
+    }
+  } else if (lane >= 2 && lane < 6) {
+    Fp u;
+    s.ld(u, S_U + (lane - 2), 0);
+    if constexpr (TABLE) slot_put(slots, VM_VOTE_T1_IN[VM_VOTE_T1_IN_U00 + (lane - 2)], u.v);
+    else slot_put(slots, VM_VOTE1_IN[VM_VOTE1_IN_U00 + (lane - 2)], u.v);
+  } else if (TABLE && lane >= 6 && lane < 9) {
+    Fp v;
+    Slab{const_cast<uint32_t*>(pk.planes), pk.cap}.ld(v, lane - 6, e);
+    if constexpr (TABLE) slot_put(slots, VM_VOTE_T1_IN[VM_VOTE_T1_IN_PK_X + (lane - 6)], v.v);
+  }
+  __syncthreads();
+  vm::run(prog.code, NPH, 64, lane, true, slots, cst, 1, vm::Out{s.p, s.cap, 0});
+  if (lane == 0) {
+    const uint32_t sf = hdr[0], pf = hdr[1];
+    const uint32_t sg_bad = sf & 1, sg_inf = (sf >> 1) & 1, sg_xz = (sf >> 2) & 1;
+    uint32_t sg_ok, sg_grp, h_inf, pk_ok = 1, pk_grp = 1;
+    if constexpr (TABLE) {
+      sg_ok = slot_flag_get(slots, VM_VOTE_T1_OUT[VM_VOTE_T1_OUT_SIG_OK]);
+      sg_grp = slot_flag_get(slots, VM_VOTE_T1_OUT[VM_VOTE_T1_OUT_SIG_GRP]);
+      h_inf = slot_flag_get(slots, VM_VOTE_T1_OUT[VM_VOTE_T1_OUT_H_INF]);
+    } else {
+      pk_ok = slot_flag_get(slots, VM_VOTE1_OUT[VM_VOTE1_OUT_PK_OK]);
+      pk_grp = slot_flag_get(slots, VM_VOTE1_OUT[VM_VOTE1_OUT_PK_GRP]);
+      sg_ok = slot_flag_get(slots, VM_VOTE1_OUT[VM_VOTE1_OUT_SIG_OK]);
+      sg_grp = slot_flag_get(slots, VM_VOTE1_OUT[VM_VOTE1_OUT_SIG_GRP]);
+      h_inf = slot_flag_get(slots, VM_VOTE1_OUT[VM_VOTE1_OUT_H_INF]);
+    }
+    // key flags in the table's terms, then the precedence of k_vm_vote_t (consensus.rs:397-416)
+    uint32_t kf = pf;
+    if (!TABLE) {
+      const uint32_t pk_bad = pf & 1, pk_inf = (pf >> 1) & 1, pk_xz = (pf >> 2) & 1;
+      kf = (pk_bad || (!pk_inf && (!pk_ok || pk_xz))) ? PKF_PARSE : pk_inf ? PKF_INF : !pk_grp ? PKF_GRP : 0u;
+    }
+    int32_t c;
+    if (kf & PKF_PARSE) c = OVH_ERR_PUBKEY;
+    else if (sg_bad) c = BLST_BAD_ENCODING;
+    else if (!sg_inf && !sg_ok) c = BLST_POINT_NOT_ON_CURVE;
+    else if (!sg_inf && (sg_xz || !sg_grp)) c = BLST_POINT_NOT_IN_GROUP;
+    else if (kf & PKF_INF) c = BLST_PK_IS_INFINITY;
+    else if (kf & PKF_GRP) c = BLST_POINT_NOT_IN_GROUP;
+    else if (h_inf || sg_inf) c = BLST_VERIFY_FAIL;
+    else c = 0;
+    *code = c;
+  }
+}
+
+// FE(f) == 1 for the standalone vote (skipped when its code is already an error): *verdict,
+// and code BLST_VERIFY_FAIL when the pairing check fails.
+__global__ __launch_bounds__(64) void k_vm_final1(VmDev prog, const uint32_t* __restrict__ cst_g, Slab F,
+                                                  int32_t* __restrict__ code, int32_t* __restrict__ verdict) {
+  if (*code != 0) {
+    if (threadIdx.x == 0) *verdict = 0;
+    return;
+  }
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  uint32_t* slots = lds + SLOT_BASE_W;
+  const uint32_t lane = threadIdx.x;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (lane < 12) {
+    Fp v;
+    F.ld(v, lane, 0);
+    slot_put(slots, VM_FINAL1_IN[lane], v.v);
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_FINAL1_NPHASES, VM_FINAL1_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  if (lane == 0) {
+    const bool ok = slot_flag_get(slots, VM_FINAL1_OUT[0]) != 0;
+    *verdict = ok ? 1 : 0;
+    if (!ok) *code = BLST_VERIFY_FAIL;
+  }
+}
+
 // The final program on one unit given as (F planes, S planes) at index u (the other three
 // partials are the identity): prod F * Miller(-G1, S) -> FE == 1.
 __device__ __forceinline__ bool final_one(uint32_t u, const VmDev& prog, const uint32_t* __restrict__ cst_g, Slab inF,
@@ -1168,7 +1285,7 @@ struct ovh_ctx {
   uint64_t slot_seed[OVH_BATCH_SLOTS] = {}, slot_base[OVH_BATCH_SLOTS] = {};
   // Fp-VM programs + constant table in device memory
   VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{},
-      vm_pkchk{}, vm_g1padd{}, vm_sign0{}, vm_sign1{};
+      vm_pkchk{}, vm_g1padd{}, vm_sign0{}, vm_sign1{}, vm_vote1{}, vm_vote_t1{}, vm_final1{};
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
@@ -1208,12 +1325,16 @@ static_assert(VM_MADD_W == VM_PADD_W && VM_HDBL1_W == VM_HDBL2_W && VM_HDBL1_W =
                   VM_HDBL1_W == VM_HDBL16_W && VM_MADD_NIN == 10 && VM_PADD_NIN == 12 && VM_HDBL1_NIN == 12,
               "MSM program shapes (tools/fpvm/progs.py)");
 static constexpr size_t LDS_SIGCHK = ((size_t)SLOT_BASE_W + (64 / VM_SIGCHK_W) * (size_t)SIGCHK_STRIDE_W) * 4;
+static constexpr uint32_t VOTE1_NSLOTS = VM_VOTE1_NSLOTS > VM_VOTE_T1_NSLOTS ? VM_VOTE1_NSLOTS : VM_VOTE_T1_NSLOTS;
+static constexpr size_t LDS_VOTE1 = ((size_t)SLOT_BASE_W + VOTE1_NSLOTS * 12 + 4) * 4;
+static constexpr size_t LDS_FINAL1 = ((size_t)SLOT_BASE_W + (size_t)VM_FINAL1_NSLOTS * 12) * 4;
 static constexpr size_t LDS_SIGN = ((size_t)SLOT_BASE_W + (64 / VM_SIGN0_W) * (size_t)SIGN_STRIDE_W) * 4;
 static constexpr size_t LDS_PKCHK = ((size_t)SLOT_BASE_W + (64 / VM_PKCHK_W) * (size_t)PKCHK_STRIDE_W) * 4;
 static constexpr uint32_t G1PADD_STRIDE_W = align128w(VM_G1PADD_NSLOTS * 12);
 static constexpr size_t LDS_G1PADD = ((size_t)SLOT_BASE_W + (64 / VM_G1PADD_W) * (size_t)G1PADD_STRIDE_W) * 4;
 static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024 && LDS_SIGCHK <= 64 * 1024 &&
-                  LDS_PKCHK <= 64 * 1024 && LDS_G1PADD <= 64 * 1024 && LDS_SIGN <= 64 * 1024 && VM_G1PADD_NIN == 6,
+                  LDS_PKCHK <= 64 * 1024 && LDS_G1PADD <= 64 * 1024 && LDS_SIGN <= 64 * 1024 &&
+                  LDS_VOTE1 <= 64 * 1024 && LDS_FINAL1 <= 64 * 1024 && VM_G1PADD_NIN == 6,
               "default LDS limit");
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
@@ -1270,6 +1391,12 @@ static int vm_init(ovh_ctx* c) {
                 VM_SIGCHK_NIN, VM_SIGCHK_OUT, VM_SIGCHK_NOUT));
   CHK(vm_upload(c, c->vm_pkchk, VM_PKCHK_CODE, VM_PKCHK_NPHASES, VM_PKCHK_W, VM_PKCHK_NW, VM_PKCHK_IN, VM_PKCHK_NIN,
                 VM_PKCHK_OUT, VM_PKCHK_NOUT));
+  CHK(vm_upload(c, c->vm_vote1, VM_VOTE1_CODE, VM_VOTE1_NPHASES, VM_VOTE1_W, VM_VOTE1_NW, VM_VOTE1_IN, VM_VOTE1_NIN,
+                VM_VOTE1_OUT, VM_VOTE1_NOUT));
+  CHK(vm_upload(c, c->vm_vote_t1, VM_VOTE_T1_CODE, VM_VOTE_T1_NPHASES, VM_VOTE_T1_W, VM_VOTE_T1_NW, VM_VOTE_T1_IN,
+                VM_VOTE_T1_NIN, VM_VOTE_T1_OUT, VM_VOTE_T1_NOUT));
+  CHK(vm_upload(c, c->vm_final1, VM_FINAL1_CODE, VM_FINAL1_NPHASES, VM_FINAL1_W, VM_FINAL1_NW, VM_FINAL1_IN,
+                VM_FINAL1_NIN, VM_FINAL1_OUT, VM_FINAL1_NOUT));
   CHK(vm_upload(c, c->vm_sign0, VM_SIGN0_CODE, VM_SIGN0_NPHASES, VM_SIGN0_W, VM_SIGN0_NW, VM_SIGN0_IN, VM_SIGN0_NIN,
                 VM_SIGN0_OUT, VM_SIGN0_NOUT));
   CHK(vm_upload(c, c->vm_sign1, VM_SIGN1_CODE, VM_SIGN1_NPHASES, VM_SIGN1_W, VM_SIGN1_NW, VM_SIGN1_IN, VM_SIGN1_NIN,
@@ -1645,6 +1772,27 @@ static int side_front(ovh_ctx* c, int slot, uint32_t n, bool pipe, uint32_t unti
 
 // pipe (ovh_verify_batch_device_async): the final stream first waits (k_gate) until the next
 // batch's vote workgroups are resident.
+// One standalone vote on the main stream (k_h2f, k_vm_vote1 / k_vm_vote_t1, k_vm_final1): its
+// own pairing equation, no coefficient (section 1 of DESIGN.md). Caller holds c->mu and waits.
+static int verify_one_locked(ovh_ctx* c, const uint8_t* d_sig, const uint8_t* d_hash, KeySrc key, int32_t* d_code) {
+  CHK(ensure_cap(c, 1));
+  int slot;
+  CHK(take_slot(c, &slot));
+  c->last_n = 0;  // no partial state for ovh_batch_partial_device / fallback
+  Slab s{c->state_slot[slot], c->cap};
+  hipStream_t st = c->stream;
+  k_h2f<<<1, WG, 0, st>>>(1, d_hash, c->xmd, s);
+  if (key.bytes)
+    k_vm_vote1<false><<<1, 64, LDS_VOTE1, st>>>(c->vm_vote1, c->vm_consts, key.bytes, PkSrc{}, d_sig, s, d_code);
+  else
+    k_vm_vote1<true><<<1, 64, LDS_VOTE1, st>>>(c->vm_vote_t1, c->vm_consts, nullptr, key.pts, d_sig, s, d_code);
+  k_vm_final1<<<1, 64, LDS_FINAL1, st>>>(c->vm_final1, c->vm_consts, Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap},
+                                          d_code, c->result + RES_BATCH + slot);
+  HIPCHK(hipEventRecord(c->ev_back[slot], st));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
                                int32_t* d_codes, bool pipe = false) {
   CHK(ensure_cap(c, n));
@@ -1716,7 +1864,8 @@ static int verify_host_locked(ovh_ctx* c, size_t n, const uint8_t* sigs, const u
     HIPCHK(hipMemcpyAsync(di, idx.data(), n * 4, hipMemcpyHostToDevice, c->stream));
     key = KeySrc{nullptr, PkSrc{c->tab.planes, c->tab.cap, c->tab.flags, di}};
   }
-  CHK(verify_async_locked(c, n, d, d + n * 96, key, dc));
+  if (n == 1) CHK(verify_one_locked(c, d, d + 96, key, dc));
+  else CHK(verify_async_locked(c, n, d, d + n * 96, key, dc));
   CHK(sync_all(c));
   HIPCHK(hipMemcpyAsync(codes, dc, 4 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -2144,8 +2293,8 @@ int ovh_verify(ovh_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* ha
   std::lock_guard<std::mutex> g(s->mu);
   HIPCHK(hipSetDevice(s->device));
   if (fixed) {
-    // the batch path at n = 1 (the Fp-VM vote program + final check): its combined check is the
-    // vote's own pairing check, so a failed verdict with a clean parse is VERIFY_FAIL
+    // one standalone vote (vote1 / vote_t1 + final1): the vote's own pairing check; a failed
+    // check with a clean parse is VERIFY_FAIL (set by k_vm_final1)
     uint8_t* d;
     CHK(stage_batch(s, 1, sig, hash, pk, &d));
     int32_t* dc = (int32_t*)(d + 176);
@@ -2155,18 +2304,11 @@ int ovh_verify(ovh_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* ha
       HIPCHK(hipMemcpyAsync(dc + 1, idx.data(), 4, hipMemcpyHostToDevice, s->stream));
       key = KeySrc{nullptr, PkSrc{s->tab.planes, s->tab.cap, s->tab.flags, dc + 1}};
     }
-    CHK(ensure_cap(s, 1));
-    int slot;
-    CHK(take_slot(s, &slot));
-    CHK(batch_front(s, slot, 1, d, d + 96, key, dc, true, true));
-    CHK(enqueue_msm(s, s->stream, slot, 1, dc));
-    enqueue_final(s, s->stream, region_F(s, slot, 1), region_S(s, slot, 1), 1, s->result, msm_S(s, slot));
-    HIPCHK(hipGetLastError());
-    int32_t out[2] = {-1, -1};
-    HIPCHK(hipMemcpyAsync(&out[0], dc, 4, hipMemcpyDeviceToHost, s->stream));
-    HIPCHK(hipMemcpyAsync(&out[1], s->result, 4, hipMemcpyDeviceToHost, s->stream));
+    CHK(verify_one_locked(s, d, d + 96, key, dc));
+    int32_t out = -1;
+    HIPCHK(hipMemcpyAsync(&out, dc, 4, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
-    return out[0] != 0 ? out[0] : (out[1] == 1 ? 0 : BLST_VERIFY_FAIL);
+    return out;
   }
   // other encodings (uncompressed keys / signatures, wrong lengths): the single-lane kernel
   CHK(ensure_in(s, 32 + sig_len + pk_len + 64));
@@ -2400,7 +2542,7 @@ static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_l
   }
   HIPCHK(hipGetLastError());
   CHK(ensure_cap(c, 1));
-  CHK(verify_async_locked(c, 1, d + n * 48, d + n * 48 + 96, KeySrc{nullptr, PkSrc{c->qc_buf, c->qc_cap, qflags, nullptr}},
+  CHK(verify_one_locked(c, d + n * 48, d + n * 48 + 96, KeySrc{nullptr, PkSrc{c->qc_buf, c->qc_cap, qflags, nullptr}},
                           dc));
   CHK(sync_all(c));
   int32_t r = -1;
@@ -2610,7 +2752,9 @@ static int qc_batch_locked(ovh_ctx* c, size_t nq, const uint8_t* sigs, const uin
   k_qc_apk<<<(uint32_t)nd, 64, 0, c->stream>>>((uint32_t)nd, doff, dent, Slab{t.planes, t.cap},
                                           Slab{c->qc_buf, c->qc_cap}, qflags);
   HIPCHK(hipGetLastError());
-  CHK(verify_async_locked(c, nd, d, d + nd * 96, KeySrc{nullptr, PkSrc{c->qc_buf, c->qc_cap, qflags, nullptr}}, dc));
+  const KeySrc qk{nullptr, PkSrc{c->qc_buf, c->qc_cap, qflags, nullptr}};
+  if (nd == 1) CHK(verify_one_locked(c, d, d + 96, qk, dc));
+  else CHK(verify_async_locked(c, nd, d, d + nd * 96, qk, dc));
   CHK(sync_all(c));
   std::vector<int32_t> dcodes(nd);
   HIPCHK(hipMemcpyAsync(dcodes.data(), dc, 4 * nd, hipMemcpyDeviceToHost, c->stream));

@@ -940,50 +940,60 @@ class Alg:
         """f_{|x|,Q}(P) conjugated. Pa = (xP, yP) affine or (XP, YP, ZP) homogeneous projective
         in Fp (every line then carries the factor ZP in Fp, which the final exponentiation
         removes: no inversion); Q = (X, Y, Z) projective in E2."""
-        p = self.p
-        xP, yP = Pa[0], Pa[1]
-        ZP = Pa[2] if len(Pa) == 3 else None
-        XQ, YQ, ZQ = Q
-        m3x = -(xP + xP + xP)
-        y2 = yP + yP
-        xPZ = self.f2_mul_fp(ZQ, xP)   # xP ZQ (times ZP when projective)
-        yPZ = self.f2_mul_fp(ZQ, yP)   # yP ZQ (times ZP when projective)
-        T = Q
+        return self.miller_loop_multi([(Pa, Q)])
+
+    def miller_loop_multi(self, pairs):
+        """prod_j f_{|x|,Q_j}(P_j) conjugated, one shared f: every iteration squares f once and
+        multiplies in each pair's line (the n = 1 vote program's two pairs)."""
+        st = []
+        for Pa, Q in pairs:
+            xP, yP = Pa[0], Pa[1]
+            ZP = Pa[2] if len(Pa) == 3 else None
+            st.append({"ZP": ZP, "Q": Q, "T": Q, "m3x": -(xP + xP + xP), "y2": yP + yP,
+                       "xPZ": self.f2_mul_fp(Q[2], xP), "yPZ": self.f2_mul_fp(Q[2], yP)})
         f = None
         for b in range(62, -1, -1):
-            X, Y, Z = T
-            XX = self.f2_sqr(X)
-            YY = self.f2_sqr(Y)
-            ZZ = self.f2_sqr(Z)
-            E = self.f2_mul_c(ZZ, (12, 12))          # 3 b' Z^2
-            l0 = self.f2_sub(YY, E)
-            if ZP is not None:
-                l0 = self.f2_mul_fp(l0, ZP)
-            l1 = self.f2_mul_fp(XX, m3x)
-            YZ = self.f2_mul(Y, Z)
-            l4 = self.f2_mul_fp(YZ, y2)
-            A = self.f2_mul(X, Y)
-            Fv = self.f2_add(self.f2_dbl(E), E)
-            X3 = self.f2_dbl(self.f2_mul(A, self.f2_sub(YY, Fv)))
-            G = self.f2_add(YY, Fv)
-            Y3 = self.f2_sub(self.f2_sqr(G), self.f2_small(self.f2_sqr(E), 12))
-            Z3 = self.f2_mul_c(self.f2_mul(YY, YZ), (8, 0))
-            T = (X3, Y3, Z3)
-            if f is None:
-                f = self.f12_mul_014(self.f12_one(), l0, l1, l4)
-            else:
-                f = self.f12_mul_014(self.f12_sqr(f), l0, l1, l4)
+            lines = []
+            for d in st:
+                X, Y, Z = d["T"]
+                XX = self.f2_sqr(X)
+                YY = self.f2_sqr(Y)
+                ZZ = self.f2_sqr(Z)
+                E = self.f2_mul_c(ZZ, (12, 12))          # 3 b' Z^2
+                l0 = self.f2_sub(YY, E)
+                if d["ZP"] is not None:
+                    l0 = self.f2_mul_fp(l0, d["ZP"])
+                l1 = self.f2_mul_fp(XX, d["m3x"])
+                YZ = self.f2_mul(Y, Z)
+                l4 = self.f2_mul_fp(YZ, d["y2"])
+                A = self.f2_mul(X, Y)
+                Fv = self.f2_add(self.f2_dbl(E), E)
+                X3 = self.f2_dbl(self.f2_mul(A, self.f2_sub(YY, Fv)))
+                G = self.f2_add(YY, Fv)
+                Y3 = self.f2_sub(self.f2_sqr(G), self.f2_small(self.f2_sqr(E), 12))
+                Z3 = self.f2_mul_c(self.f2_mul(YY, YZ), (8, 0))
+                d["T"] = (X3, Y3, Z3)
+                lines.append((l0, l1, l4))
+            for k, (l0, l1, l4) in enumerate(lines):
+                if f is None:
+                    f = self.f12_mul_014(self.f12_one(), l0, l1, l4)
+                elif k == 0:
+                    f = self.f12_mul_014(self.f12_sqr(f), l0, l1, l4)
+                else:
+                    f = self.f12_mul_014(f, l0, l1, l4)
             if (X_ABS >> b) & 1:
-                X, Y, Z = T
-                th = self.f2_sub(self.f2_mul(Y, ZQ), self.f2_mul(YQ, Z))
-                lm = self.f2_sub(self.f2_mul(X, ZQ), self.f2_mul(XQ, Z))
-                l0 = self.f2_sub(self.f2_mul(th, XQ), self.f2_mul(lm, YQ))
-                if ZP is not None:
-                    l0 = self.f2_mul_fp(l0, ZP)
-                l1 = self.f2_neg(self.f2_mul(th, xPZ))
-                l4 = self.f2_mul(lm, yPZ)
-                T = self.pt_add("f2", T, Q)
-                f = self.f12_mul_014(f, l0, l1, l4)
+                for d in st:
+                    X, Y, Z = d["T"]
+                    XQ, YQ, ZQ = d["Q"]
+                    th = self.f2_sub(self.f2_mul(Y, ZQ), self.f2_mul(YQ, Z))
+                    lm = self.f2_sub(self.f2_mul(X, ZQ), self.f2_mul(XQ, Z))
+                    l0 = self.f2_sub(self.f2_mul(th, XQ), self.f2_mul(lm, YQ))
+                    if d["ZP"] is not None:
+                        l0 = self.f2_mul_fp(l0, d["ZP"])
+                    l1 = self.f2_neg(self.f2_mul(th, d["xPZ"]))
+                    l4 = self.f2_mul(lm, d["yPZ"])
+                    d["T"] = self.pt_add("f2", d["T"], d["Q"])
+                    f = self.f12_mul_014(f, l0, l1, l4)
         return self.f12_conj(f)
 
     def f12_exp_x(self, f):

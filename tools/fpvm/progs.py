@@ -7,6 +7,10 @@ layouts. Input and output names are listed in the order the HIP side addresses t
            tau = -psi^2(sigma) (affine) for the Pippenger MSM of sum r_i sigma_i
   vote_t   the same for a public key taken from the device validator table (ovh_set_validators:
            already decompressed and group-checked, projective) or a QC's aggregated key.
+  vote1    a standalone vote (ovh_verify, n = 1, scalar 1): f = Miller(pk, H) Miller(-G1, sigma)
+           as one two-pair Miller loop, so its check is final1 alone (no MSM, no partials)
+  vote_t1  the same from a table / aggregated key (a QC's verify_aggregated_signature)
+  final1   final exponentiation of f == 1
   rs       bisection only: r sigma = [a] sigma + [b] tau for one vote (the per-vote term the MSM
            sums), 32-step joint chain
   madd     MSM bucket level 0: B (projective) + A (affine)
@@ -129,6 +133,48 @@ def build_vote_t():
         p.output(name, v)
     for (name, plane), v in zip(VOTE_ST, flat12(f) + affine_pair(a, Qs)):
         p.store(name, v, plane)
+    return p
+
+
+VOTE1_ST = [(n, S_F + k) for k, n in enumerate(f12_names("f"))]
+
+
+def build_vote1(table: bool):
+    def build():
+        p = Prog("vote_t1" if table else "vote1")
+        a = Alg(p, use_sop=USE_SOP)
+        R = p.const(R_MONT)
+        if table:
+            Pa = (p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z"))
+        else:
+            pk_ok, (px, py) = a.g1_decompress(p.input("pk_x") * R, p.input("pk_sort"))
+            pk_grp, _ = a.g1_in_group((px, py, p.one))
+            Pa = (px, py)
+        sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
+        u0 = (p.input("u00"), p.input("u01"))
+        u1 = (p.input("u10"), p.input("u11"))
+        p.section = "sig"
+        sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
+        Qs = (qx, qy, (p.one, p.zero))
+        sig_grp = a.g2_in_group(Qs)
+        p.section = None
+        H = a.hash_to_g2(u0, u1)
+        h_inf = a.f2_is_zero(H[2])
+        f = a.miller_loop_multi([(Pa, H), ((p.const(G1X), p.const(-G1Y)), Qs)])
+        flags = [sig_ok, sig_grp, h_inf] if table else [pk_ok, pk_grp, sig_ok, sig_grp, h_inf]
+        for name, v in zip(VOTE_T_OUT if table else VOTE_OUT, flags):
+            p.output(name, v)
+        for (name, plane), v in zip(VOTE1_ST, flat12(f)):
+            p.store(name, v, plane)
+        return p
+    return build
+
+
+def build_final1():
+    p = Prog("final1")
+    a = Alg(p, inv_op=True, use_sop=USE_SOP)
+    F = unflat12([p.input(n) for n in f12_names("f")])
+    p.output("ok", a.f12_eq_one(a.final_exp(F)))
     return p
 
 
@@ -344,6 +390,9 @@ for _m in HDBL_M:
     PROGRAMS["hdbl%d" % _m] = (build_hdbl(_m), PA_IN + PB_IN, PT_OUT)
 PROGRAMS["sigchk"] = (build_sigchk, SIGCHK_IN, SIGCHK_OUT)
 PROGRAMS["pkchk"] = (build_pkchk, PKCHK_IN, PKCHK_OUT)
+PROGRAMS["vote1"] = (build_vote1(False), VOTE_IN, VOTE_OUT)
+PROGRAMS["vote_t1"] = (build_vote1(True), VOTE_T_IN, VOTE_T_OUT)
+PROGRAMS["final1"] = (build_final1, f12_names("f"), ["ok"])
 PROGRAMS["sign0"] = (build_sign0, SIGN0_IN, SIGN_ACC + SIGN_H)
 PROGRAMS["sign1"] = (build_sign1, SIGN_ACC + SIGN_H, SIGN_ACC)
 PROGRAMS["g1padd"] = (build_g1padd, G1A_IN + G1B_IN, G1_OUT)
