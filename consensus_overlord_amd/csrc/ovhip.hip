@@ -804,22 +804,24 @@ __global__ __launch_bounds__(64) void k_g2p_compress(Slab in, uint8_t* out) {
 }
 
 // Crypto::sign (consensus.rs:390-395) on the VM: one signature per 16-lane slice. sign0 hashes
-// to G2 (u0, u1 from k_h2f) and multiplies by the top 64 bits of the secret scalar, sign1 runs
-// three times for the rest: the scalar enters only as the selb bits of each launch, so the
-// instruction stream does not depend on it. Lane 0 of the slice compresses the result.
+// to G2 (u0, u1 from k_h2f), builds 2H, 3H and multiplies by the top 64 bits of the secret
+// scalar (2-bit windows), sign1 runs three times for the rest: the scalar enters only as the
+// selb bits of each launch, so the instruction stream does not depend on it. Lane 0 of the
+// slice compresses the result.
 constexpr uint32_t SIGN_NSLOTS = VM_SIGN0_NSLOTS > VM_SIGN1_NSLOTS ? VM_SIGN0_NSLOTS : VM_SIGN1_NSLOTS;
-constexpr uint32_t SIGN_STRIDE_W = align128w(SIGN_NSLOTS * 12 + 6 * 12);  // + H stash
+constexpr uint32_t SIGN_STRIDE_W = align128w(SIGN_NSLOTS * 12 + 24 * 12);  // + acc, H, 2H, 3H stash
 __global__ __launch_bounds__(64) void k_vm_sign(uint32_t n, VmDev p0, VmDev p1, const uint32_t* __restrict__ cst_g,
                                                 const uint8_t* __restrict__ sks, Slab s, uint8_t* __restrict__ out) {
-  static_assert(VM_SIGN0_W == VM_SIGN1_W && VM_SIGN0_NOUT == 12 && VM_SIGN1_NIN == 12 && VM_SIGN1_NOUT == 6,
+  static_assert(VM_SIGN0_W == VM_SIGN1_W && VM_SIGN0_NOUT == 24 && VM_SIGN1_NIN == 24 && VM_SIGN1_NOUT == 6,
                 "sign program shapes (tools/fpvm/progs.py)");
+  constexpr uint32_t W = VM_SIGN0_W;
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
-  const uint32_t slice = threadIdx.x / VM_SIGN0_W, lane = threadIdx.x % VM_SIGN0_W;
+  const uint32_t slice = threadIdx.x / W, lane = threadIdx.x % W;
   uint32_t* slots = lds + SLOT_BASE_W + slice * SIGN_STRIDE_W;
-  uint32_t* hst = slots + SIGN_NSLOTS * 12;
-  const uint32_t i = blockIdx.x * (64 / VM_SIGN0_W) + slice;
+  uint32_t* hst = slots + SIGN_NSLOTS * 12;  // 24 values: acc (6), H, 2H, 3H (18)
+  const uint32_t i = blockIdx.x * (64 / W) + slice;
   const bool active = i < n;
   load_consts(cst, cst_g, VM_NCONST);
   uint64_t k[4] = {0, 0, 0, 0};  // big-endian 64-bit chunks, k[0] the most significant
@@ -834,30 +836,25 @@ __global__ __launch_bounds__(64) void k_vm_sign(uint32_t n, VmDev p0, VmDev p1, 
     }
   }
   __syncthreads();
-  vm::run(p0.code, VM_SIGN0_NPHASES, VM_SIGN0_W, lane, active, slots, cst, k[0], vm::Out{nullptr, 0, 0});
+  vm::run(p0.code, VM_SIGN0_NPHASES, W, lane, active, slots, cst, k[0], vm::Out{nullptr, 0, 0});
   __syncthreads();
-  uint32_t v[12];
-  if (active && lane < 12) {
-    const uint32_t src = VM_SIGN0_OUT[lane];
-    for (int l = 0; l < 12; ++l) v[l] = slots[src * 12 + l];
-    if (lane >= 6)
-      for (int l = 0; l < 12; ++l) hst[(lane - 6) * 12 + l] = v[l];
-  }
+  if (active)
+    for (uint32_t q = lane; q < 24; q += W)
+      for (int l = 0; l < 12; ++l) hst[q * 12 + l] = slots[VM_SIGN0_OUT[q] * 12 + l];
   __syncthreads();
   for (int r = 1; r < 4; ++r) {
-    if (active && lane < 12) slot_put(slots, VM_SIGN1_IN[lane], lane < 6 ? v : hst + (lane - 6) * 12);
+    if (active)
+      for (uint32_t q = lane; q < 24; q += W) slot_put(slots, VM_SIGN1_IN[q], hst + q * 12);
     __syncthreads();
-    vm::run(p1.code, VM_SIGN1_NPHASES, VM_SIGN1_W, lane, active, slots, cst, k[r], vm::Out{nullptr, 0, 0});
+    vm::run(p1.code, VM_SIGN1_NPHASES, W, lane, active, slots, cst, k[r], vm::Out{nullptr, 0, 0});
     __syncthreads();
-    if (active && lane < 6) {
-      const uint32_t src = VM_SIGN1_OUT[lane];
-      for (int l = 0; l < 12; ++l) v[l] = slots[src * 12 + l];
-    }
+    if (active && lane < 6)
+      for (int l = 0; l < 12; ++l) hst[lane * 12 + l] = slots[VM_SIGN1_OUT[lane] * 12 + l];
     __syncthreads();
   }
   if (active && lane < 6) {
     Fp t;
-    for (int l = 0; l < 12; ++l) t.v[l] = v[l];
+    for (int l = 0; l < 12; ++l) t.v[l] = hst[lane * 12 + l];
     vm::canon(t, t);
     for (int l = 0; l < 12; ++l) hst[lane * 12 + l] = t.v[l];
   }

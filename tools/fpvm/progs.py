@@ -293,30 +293,41 @@ def build_g1padd():
     return p
 
 
-def _smul64(a, acc, H, first=False):
-    """MSB-first double-and-add over the launch scalar's 64 bits (complete formulas, selb)."""
-    start = 63
-    if first:   # acc = O: the top bit only selects
-        acc = a.pt_selb("f2", 63, acc, H)
-        start = 62
-    for b in range(start, -1, -1):
-        acc = a.pt_dbl("f2", acc)
-        acc = a.pt_selb("f2", b, acc, a.pt_add("f2", acc, H))
+def _smul64(a, acc, T, first=False):
+    """acc -> [2^64] acc + [k] H over the launch scalar's 64 bits k, 2-bit windows MSB first:
+    two doublings and one complete addition of T[v] (T = H, 2H, 3H; v = 0 adds the identity,
+    picked by two selb levels off the doubling chain)."""
+    H, H2, H3 = T
+    p = a.p
+    O = ((p.zero, p.zero), (p.one, p.zero), (p.zero, p.zero))
+    for w in range(31, -1, -1):
+        # the window's addend is selected once the previous window's sum exists
+        dep = None if (first and w == 31) else acc[2][0]
+        lo = a.pt_selb("f2", 2 * w, O, H, dep)
+        hi = a.pt_selb("f2", 2 * w, H2, H3, dep)
+        ad = a.pt_selb("f2", 2 * w + 1, lo, hi, dep)
+        if first and w == 31:
+            acc = ad
+            continue
+        acc = a.pt_dbl("f2", a.pt_dbl("f2", acc))
+        acc = a.pt_add("f2", acc, ad)
     return acc
 
 
 SIGN0_IN = ["u00", "u01", "u10", "u11"]
 SIGN_ACC = ["c%d" % k for k in range(6)]
-SIGN_H = ["h%d" % k for k in range(6)]
+SIGN_H = ["h%d" % k for k in range(18)]   # H, 2H, 3H (projective)
 
 
 def build_sign0():
     p = Prog("sign0")
     a = Alg(p, use_sop=USE_SOP)
     H = a.hash_to_g2((p.input("u00"), p.input("u01")), (p.input("u10"), p.input("u11")))
+    H2 = a.pt_dbl("f2", H)
+    H3 = a.pt_add("f2", H2, H)
     O = ((p.zero, p.zero), (p.one, p.zero), (p.zero, p.zero))
-    acc = _smul64(a, O, H, first=True)
-    for name, v in zip(SIGN_ACC + SIGN_H, flat_g2p(acc) + flat_g2p(H)):
+    acc = _smul64(a, O, (H, H2, H3), first=True)
+    for name, v in zip(SIGN_ACC + SIGN_H, flat_g2p(acc) + flat_g2p(H) + flat_g2p(H2) + flat_g2p(H3)):
         p.output(name, v)
     return p
 
@@ -325,8 +336,8 @@ def build_sign1():
     p = Prog("sign1")
     a = Alg(p, use_sop=USE_SOP)
     acc = _pt_in(p, SIGN_ACC)
-    H = _pt_in(p, SIGN_H)
-    for name, v in zip(SIGN_ACC, flat_g2p(_smul64(a, acc, H))):
+    T = tuple(unflat_g2p([p.input(n) for n in SIGN_H[6 * j:6 * j + 6]]) for j in range(3))
+    for name, v in zip(SIGN_ACC, flat_g2p(_smul64(a, acc, T))):
         p.output(name, v)
     return p
 
