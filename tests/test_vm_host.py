@@ -201,3 +201,38 @@ def test_fp_inv(hx):
                          out.ctypes.data_as(u32p))
         got = sum(int(w) << (32 * k) for k, w in enumerate(out))
         assert got == (pow(a, -1, P) if a else 0), hex(a)
+
+
+@pytest.mark.parametrize("any_all", [0, 1])
+def test_percall_programs_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
+    """The per-call programs through the interpreter == simulator: sigchk / pkchk on golden
+    signatures and keys (a non-subgroup case included), g1padd, sign0 + sign1 over a golden
+    key's scalar chunks, and vote1 / vote_t1 + final1 on a golden vote (gen.check ties each to
+    the oracle: decompressed points, sums, the golden signature, the pairing verdict)."""
+    consts, progs_ = built
+    bls = gen._oracle()
+    with open(os.path.join(ROOT, "tests", "golden", "golden_v1.json")) as fh:
+        g = json.load(fh)
+
+    def run(name, inp, scalar=0):
+        _, sc, words, _, _ = progs_[name]
+        sim = sched.simulate(sc, words, inp, scalar)
+        assert_same(run_vm(hx, consts, sc, words, inp, scalar, any_all), sim, name)
+        return sim
+    for inp in golden_votes:
+        run("sigchk", {n: inp[n] for n in progs.SIGCHK_IN})
+        run("pkchk", {n: inp[n] for n in progs.PKCHK_IN})
+    A, B = (bls.g1_from_bytes(bytes.fromhex(k["pk"])) for k in g["keys"][:2])
+    run("g1padd", dict(zip(progs.G1A_IN + progs.G1B_IN, [A[0] * 3 % P, A[1] * 3 % P, 3, B[0], B[1], 1])))
+    sk = int(g["keys"][0]["sk"], 16)
+    chunks = [(sk >> (64 * j)) & (2 ** 64 - 1) for j in (3, 2, 1, 0)]
+    inp = golden_votes[0]
+    o = run("sign0", {n: inp[n] for n in progs.SIGN0_IN}, chunks[0])
+    run("sign1", {n: o[n] for n in progs.SIGN_ACC + progs.SIGN_H}, chunks[1])
+    o = run("vote1", inp, 1)
+    fin = {"f%d" % j: o["st:f%d" % j] for j in range(12)}
+    assert run("final1", fin) == {"ok": 1}
+    pk = bls.g1_from_bytes(bytes.fromhex(g["keys"][0]["pk"]))
+    tin = {n: inp[n] for n in ("sig_x0", "sig_x1", "sig_sort", "u00", "u01", "u10", "u11")}
+    tin.update(pk_X=pk[0] * 5 % P, pk_Y=pk[1] * 5 % P, pk_Z=5)
+    run("vote_t1", tin, 1)
