@@ -36,12 +36,6 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-# Hardware queues per process (HIP's default is 4). libovhip runs three streams (per-vote stages,
-# two final streams); torch's stream and the process group's RCCL stream come on top at N > 1.
-# With four queues two of those streams share one queue and run in order, which put the
-# final-stream work of the multi-GPU path back in line with the vote kernels (r02ae trace:
-# 814k instead of 1,008k verifs/s at one rank). Set before HIP initialises (torch import).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 sys.path.insert(0, ROOT)
 
 SEED = 0xC17A
@@ -56,6 +50,7 @@ OVH_FLAG_PROFILE = 0x2
 PEAK_MAD_U64 = 2.9143e13
 PEAK_FULLRATE = 256 * 4 * 32 * 2.4e9
 W_V_CANON = 18300   # algorithmic Montgomery products per verification
+W_MSM = 350         # the Pippenger share of sum r_i sigma_i (the k_msm_* kernels)
 STAGE_TO_WORK = {"hash_to_field": "hash_to_field", "vote": "vote", "fold": "fold_per_partial",
                  "final": "final_per_batch", "fallback": "fallback"}
 PER_BATCH_STAGES = {"final"}
@@ -80,6 +75,31 @@ def synth_inputs(lib, lo: int, n: int):
     return sks, hs
 
 
+def cpu_allowance():
+    """CPUs this process may use: its affinity mask, capped by the cgroup CPU quota (cgroup v2
+    cpu.max / v1 cfs_quota_us) -- on a shared GPU box the mask may list the whole machine while
+    the quota grants a share of it."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+                q = int(fh.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+                per = int(fh.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    n = aff if quota is None else max(1, min(aff, int(quota)))
+    return n, {"affinity_cpus": aff, "cgroup_quota_cpus": quota}
+
+
 def cpu_baseline(sigs: np.ndarray, hs: np.ndarray, pks: np.ndarray, budget_s: float):
     """The CPU oracle's C restatement (oracle/c/bls_oracle.c, 6x64-bit limbs; NOT blst) on the
     host cores, on the same 4096-vote workload: (a) the RLC batch verify over all the threads
@@ -87,7 +107,7 @@ def cpu_baseline(sigs: np.ndarray, hs: np.ndarray, pks: np.ndarray, budget_s: fl
     vote, serial, one thread (consensus.rs:397-416) -- on a bounded prefix of the votes."""
     sys.path.insert(0, os.path.join(ROOT, "oracle", "py"))
     import orc
-    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1), 64))
+    threads, cpu_info = cpu_allowance()
     t0 = time.perf_counter()
     codes, ok = orc.verify_batch_rlc(sigs, hs, pks, seed=0xC17A, threads=threads)
     dt_b = time.perf_counter() - t0
@@ -109,9 +129,10 @@ def cpu_baseline(sigs: np.ndarray, hs: np.ndarray, pks: np.ndarray, budget_s: fl
     except OSError:
         pass
     return {"value": round(len(sigs) / dt_b, 2), "unit": "verifications/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "host_cpus": os.cpu_count(),
-            "sample": "all %d votes of the workload, RLC batch verify on %d threads (C restatement "
-                      "oracle/c/bls_oracle.c, not blst), %.2f s" % (len(sigs), threads, dt_b),
+            "per_core": round(len(sigs) / dt_b / threads, 2),
+            "cpu_model": model, "host_cpus": os.cpu_count(), "allowance": cpu_info,
+            "sample": "all %d votes of the workload, RLC batch verify on %d threads = every CPU this job may "
+                      "run on (C restatement oracle/c/bls_oracle.c, not blst), %.2f s" % (len(sigs), threads, dt_b),
             "serial_1core": {"value": round(n1 / dt_1, 2), "cores": 1,
                              "sample": "first %d votes, per-vote verify_signature serially (the reference's "
                                        "call shape), %.2f s" % (n1, dt_1)}}
@@ -332,9 +353,10 @@ def main():
             if tk is not None and B == 4096:
                 traffic = tk["hbm_bytes_per_launch"]
         # algorithmic work of the dominant stage: SURVEY.md 8(d) canonical W_v = 18,300 M per vote
-        # (Appendix C) less the Fp12 merge (54 M) and the amortised final exponentiation (4 M),
-        # which other kernels do; the program's own count (vote program) is reported beside it
-        canon = {"vote": W_V_CANON - 54 - 4}
+        # (Appendix C) less the Pippenger MSM share (350 M), the Fp12 merge (54 M) and the
+        # amortised final exponentiation (4 M), which other kernels do; the program's own count
+        # (vote program) is reported beside it, and the MSM kernels' own fraction below
+        canon = {"vote": W_V_CANON - W_MSM - 54 - 4}
         work_M = canon.get(dname, Mu[STAGE_TO_WORK[dname]])
         macs = work_M * units * macs_per_M
         achieved = macs / (avg_ms[dom] * 1e-3) / 1e12
@@ -367,12 +389,15 @@ def main():
                 "frac": round(achieved * 1e12 / PEAK_MAD_U64, 4),
                 "frac_of_fullrate_valu": round(achieved * 1e12 / PEAK_FULLRATE, 4),
                 "work_M_per_unit": work_M,
-                "work_basis": "SURVEY 8(d) canonical W_v minus merge + amortised FE" if dname in canon
+                "work_basis": "SURVEY 8(d) canonical W_v minus MSM + merge + amortised FE" if dname in canon
                               else "program heavy ops (workmodel.json)",
                 "program_M_per_unit": Mu[STAGE_TO_WORK[dname]],
                 "program_frac": round(prog_achieved * 1e12 / PEAK_MAD_U64, 4),
                 "traffic": traffic,
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x 2 + WRITE_SIZE, pmc_traffic.json)",
+                "msm": ({"ms": round(float(avg_ms[names.index("msm")]), 4), "work_M_per_unit": W_MSM,
+                         "frac": round(W_MSM * B * macs_per_M / (avg_ms[names.index("msm")] * 1e-3) / PEAK_MAD_U64, 4)}
+                        if avg_ms[names.index("msm")] > 0 else None),
                 "path_M_per_vote": round(path_M, 1),
                 "path_frac": round(value / world * path_M * macs_per_M / PEAK_MAD_U64, 4),
             },

@@ -66,6 +66,12 @@ struct Sha256 {
   }
 };
 
+// zero secret intermediates (volatile stores: not removed as dead by the optimiser)
+inline void wipe(void* p, size_t n) {
+  volatile uint8_t* q = (volatile uint8_t*)p;
+  while (n--) *q++ = 0;
+}
+
 inline void sha256(uint8_t out[32], const uint8_t* m, size_t n) {
   Sha256 h;
   h.update(m, n);
@@ -89,6 +95,9 @@ inline void hmac(uint8_t out[32], const uint8_t* key, size_t klen, const uint8_t
   ho.update(pad, 64);
   ho.update(inner, 32);
   ho.final(out);
+  wipe(k, sizeof k);
+  wipe(pad, sizeof pad);
+  wipe(inner, sizeof inner);
 }
 
 // RFC 5869 HKDF-Expand with SHA-256, L <= 255 * 32.
@@ -104,6 +113,8 @@ inline void hkdf_expand(uint8_t* okm, size_t L, const uint8_t prk[32], const uin
     memcpy(okm + done, t, k);
     done += k;
   }
+  wipe(t, sizeof t);
+  wipe(prev, sizeof prev);
 }
 
 static const uint8_t R_BE[32] = {0x73, 0xed, 0xa7, 0x53, 0x29, 0x9d, 0x7d, 0x48, 0x33, 0x39, 0xd8,
@@ -142,6 +153,7 @@ inline void be_mod_r(uint8_t out[32], const uint8_t* in, size_t n) {
     }
   }
   memcpy(out, acc + 1, 32);
+  wipe(acc, sizeof acc);
 }
 
 inline bool is_zero32(const uint8_t* a) {
@@ -162,6 +174,8 @@ inline bool key_gen(uint8_t sk_be[32], const uint8_t* ikm, size_t ilen) {
     hmac(prk, salt, 32, ikm, ilen, ZERO1, 1);  // HKDF-Extract(salt, IKM || I2OSP(0, 1))
     hkdf_expand(okm, 48, prk, L2, 2);         // info = key_info ("") || I2OSP(L, 2)
     be_mod_r(sk_be, okm, 48);
+    wipe(prk, sizeof prk);
+    wipe(okm, sizeof okm);
     if (!is_zero32(sk_be)) return true;
     sha256(salt, salt, 32);
   }

@@ -151,8 +151,14 @@ __global__ __launch_bounds__(WG) void k_vote_digest(uint32_t n, const uint64_t* 
   if (i >= n) return;
   uint8_t h[VOTE_HASH_MAX];
   const uint32_t len = lens[i];
-  for (uint32_t k = 0; k < len; ++k) h[k] = bh[(size_t)i * VOTE_HASH_MAX + k];
   uint8_t d[32];
+  if (len > VOTE_HASH_MAX) {
+    // lengths live in device memory (ovh_vote_digests_device cannot reject them on the host):
+    // an over-long block hash gets the all-zero digest, which no vote hash equals
+    for (int k = 0; k < 32; ++k) out[(size_t)i * 32 + k] = 0;
+    return;
+  }
+  for (uint32_t k = 0; k < len; ++k) h[k] = bh[(size_t)i * VOTE_HASH_MAX + k];
   vote_digest(d, heights[i], rounds[i], types[i], h, len);
   for (int k = 0; k < 32; ++k) out[(size_t)i * 32 + k] = d[k];
 }
@@ -1232,7 +1238,7 @@ struct ovh_ctx {
   // Batches alternate between two final streams, so two finals may run at once (each shares a
   // SIMD with a vote wave and takes longer than a vote kernel there).
   hipStream_t fstream = nullptr, fstream2 = nullptr;
-  hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse)
+  hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse; lazy)
   hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
@@ -1257,7 +1263,7 @@ struct ovh_ctx {
   uint32_t scr_cap = 0;
   uint32_t* comb = nullptr;  // ovh_combine_partials_device scratch
   uint32_t comb_cap = 0;
-  uint32_t* part_out = nullptr;  // multi-device: this device's partial (216 words)
+  uint32_t* part_out = nullptr;  // multi-device: this device's partials (2 x 216 words: table / other votes)
   int32_t* result = nullptr;     // device verdict words
   unsigned long long* vstart = nullptr;  // vote workgroups started (k_gate), device
   uint64_t vlaunched = 0;                // vote workgroups launched, host
@@ -1833,39 +1839,100 @@ static int stage_batch(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t*
   return 0;
 }
 
-// The table entry of each voter (all found: true, idx filled) -- the vote_t path.
-static bool table_lookup(ovh_ctx* c, size_t n, const uint8_t* pks, std::vector<int32_t>& idx) {
-  if (!c->tab.n) return false;
-  idx.resize(n);
+// The validator-table entry of each voter: votes whose key is in the table run the vote_t
+// program (no key decompression / subgroup check), the others the vote program. perm lists the
+// votes table-first (perm[j] = the caller's index of staged vote j), idx the table entry of each
+// staged table vote; returns the number of table votes. perm stays empty when no reordering is
+// needed (no table vote, or every vote in the table).
+static size_t table_split(ovh_ctx* c, size_t n, const uint8_t* pks, std::vector<uint32_t>& perm,
+                          std::vector<int32_t>& idx) {
+  perm.clear();
+  idx.clear();
+  if (!c->tab.n) return 0;
+  std::vector<int32_t> e(n);
   std::string k(48, '\0');
+  size_t t = 0;
   for (size_t i = 0; i < n; ++i) {
     memcpy(&k[0], pks + 48 * i, 48);
     auto it = c->tab.index.find(k);
-    if (it == c->tab.index.end()) return false;
-    idx[i] = (int32_t)it->second;
+    e[i] = it == c->tab.index.end() ? -1 : (int32_t)it->second;
+    t += e[i] >= 0;
   }
-  return true;
+  if (t == n) {
+    idx = std::move(e);
+    return n;
+  }
+  if (t == 0) return 0;
+  perm.reserve(n);
+  for (size_t i = 0; i < n; ++i)
+    if (e[i] >= 0) {
+      perm.push_back((uint32_t)i);
+      idx.push_back(e[i]);
+    }
+  for (size_t i = 0; i < n; ++i)
+    if (e[i] < 0) perm.push_back((uint32_t)i);
+  return t;
 }
 
-// ovh_verify_batch on one device (caller holds c->mu): codes (host) of n votes.
+// Host inputs of n votes staged table-first (table_split) on the main stream: sigs | hashes |
+// pks | codes | table indices. *t = the number of table votes; perm as table_split.
+static int stage_split(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                       uint8_t** d, size_t* t, std::vector<uint32_t>& perm) {
+  std::vector<int32_t> idx;
+  *t = table_split(c, n, pks, perm, idx);
+  if (perm.empty()) {
+    CHK(stage_batch(c, n, sigs, hashes, pks, d));
+  } else {
+    std::vector<uint8_t> h(n * 176);
+    for (size_t j = 0; j < n; ++j) {
+      const size_t i = perm[j];
+      memcpy(&h[96 * j], sigs + 96 * i, 96);
+      memcpy(&h[n * 96 + 32 * j], hashes + 32 * i, 32);
+      memcpy(&h[n * 128 + 48 * j], pks + 48 * i, 48);
+    }
+    CHK(stage_batch(c, n, h.data(), h.data() + n * 96, h.data() + n * 128, d));
+    HIPCHK(hipStreamSynchronize(c->stream));  // the pageable copy of h completed before h dies
+  }
+  if (*t) HIPCHK(hipMemcpyAsync(*d + n * 180, idx.data(), *t * 4, hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
+// The key source of staged votes [lo, lo + cnt): the table for lo < t, else the key bytes.
+static KeySrc staged_key(ovh_ctx* c, size_t n, uint8_t* d, size_t t, size_t lo) {
+  if (lo < t) return KeySrc{nullptr, PkSrc{c->tab.planes, c->tab.cap, c->tab.flags, (int32_t*)(d + n * 180) + lo}};
+  return KeySrc{d + n * 128 + 48 * lo, PkSrc{}};
+}
+
+// ovh_verify_batch on one device (caller holds c->mu): codes (host) of n votes. Table votes and
+// the others run as two batches (each its own combined check) when a batch mixes them.
 static int verify_host_locked(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
                               int32_t* codes) {
   HIPCHK(hipSetDevice(c->device));
+  CHK(ensure_in(c, n * (96 + 32 + 48 + 4 + 4) + 64));
   uint8_t* d;
-  CHK(stage_batch(c, n, sigs, hashes, pks, &d));
+  size_t t;
+  std::vector<uint32_t> perm;
+  CHK(stage_split(c, n, sigs, hashes, pks, &d, &t, perm));
   int32_t* dc = (int32_t*)(d + n * 176);
-  std::vector<int32_t> idx;
-  KeySrc key{d + n * 128, PkSrc{}};
-  if (table_lookup(c, n, pks, idx)) {
-    int32_t* di = dc + n;
-    HIPCHK(hipMemcpyAsync(di, idx.data(), n * 4, hipMemcpyHostToDevice, c->stream));
-    key = KeySrc{nullptr, PkSrc{c->tab.planes, c->tab.cap, c->tab.flags, di}};
+  if (n == 1) {
+    CHK(verify_one_locked(c, d, d + 96, staged_key(c, n, d, t, 0), dc));
+  } else {
+    for (size_t lo : {(size_t)0, t}) {
+      const size_t cnt = lo == 0 ? t : n - t;
+      if (!cnt) continue;
+      CHK(verify_async_locked(c, cnt, d + 96 * lo, d + n * 96 + 32 * lo, staged_key(c, n, d, t, lo), dc + lo));
+    }
   }
-  if (n == 1) CHK(verify_one_locked(c, d, d + 96, key, dc));
-  else CHK(verify_async_locked(c, n, d, d + n * 96, key, dc));
   CHK(sync_all(c));
-  HIPCHK(hipMemcpyAsync(codes, dc, 4 * n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  if (perm.empty()) {
+    HIPCHK(hipMemcpyAsync(codes, dc, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+  } else {
+    std::vector<int32_t> pc(n);
+    HIPCHK(hipMemcpyAsync(pc.data(), dc, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (size_t j = 0; j < n; ++j) codes[perm[j]] = pc[j];
+  }
   return 0;
 }
 
@@ -1899,8 +1966,15 @@ static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
   locks.emplace_back(root->mu);
   for (ovh_ctx* s : root->sub) locks.emplace_back(s->mu);
   ovh_ctx* s0 = root->sub[0];
-  std::vector<int> slot(nd, 0);
+  // per device: its shard, staged table-first (stage_split), as up to two parts (table votes,
+  // other votes), each a batch with its own partial
+  struct Part {
+    int slot;
+    size_t lo, cnt;
+  };
+  std::vector<std::vector<Part>> parts(nd);
   std::vector<int32_t*> dcodes(nd, nullptr);
+  std::vector<std::vector<uint32_t>> perms(nd);
   size_t k = 0;
   for (size_t d = 0; d < nd; ++d) {
     ovh_ctx* s = root->sub[d];
@@ -1908,26 +1982,29 @@ static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
     shard_range(n, nd, d, &lo, &cnt);
     if (!cnt) continue;
     HIPCHK(hipSetDevice(s->device));
+    CHK(ensure_in(s, cnt * (96 + 32 + 48 + 4 + 4) + 64));
     uint8_t* in;
-    CHK(stage_batch(s, cnt, sigs + lo * 96, hashes + lo * 32, pks + lo * 48, &in));
+    size_t t;
+    CHK(stage_split(s, cnt, sigs + lo * 96, hashes + lo * 32, pks + lo * 48, &in, &t, perms[d]));
     dcodes[d] = (int32_t*)(in + cnt * 176);
-    std::vector<int32_t> idx;
-    KeySrc key{in + cnt * 128, PkSrc{}};
-    if (table_lookup(s, cnt, pks + lo * 48, idx)) {
-      int32_t* di = dcodes[d] + cnt;
-      HIPCHK(hipMemcpyAsync(di, idx.data(), cnt * 4, hipMemcpyHostToDevice, s->stream));
-      key = KeySrc{nullptr, PkSrc{s->tab.planes, s->tab.cap, s->tab.flags, di}};
-    }
     CHK(ensure_cap(s, cnt));
-    CHK(take_slot(s, &slot[d]));
-    s->test_base = root->test_base + lo;  // OVH_FLAG_TEST_RLC only: one global index per vote
-    CHK(batch_front(s, slot[d], (uint32_t)cnt, in, in + cnt * 96, key, dcodes[d]));
-    CHK(shard_partial(s, slot[d], (uint32_t)cnt, dcodes[d], s->part_out, nullptr));
-    // partial -> devices[0] (peer copy over xGMI), ordered on this device's stream
-    HIPCHK(hipMemcpyPeerAsync(root->gather + k * OVH_PARTIAL_BYTES, s0->device, s->part_out, s->device,
-                              OVH_PARTIAL_BYTES, s->stream));
+    for (size_t plo : {(size_t)0, t}) {
+      const size_t pc = plo == 0 ? t : cnt - t;
+      if (!pc) continue;
+      Part p{0, plo, pc};
+      CHK(take_slot(s, &p.slot));
+      s->test_base = root->test_base + lo + plo;  // OVH_FLAG_TEST_RLC only: one global index per vote
+      CHK(batch_front(s, p.slot, (uint32_t)pc, in + 96 * plo, in + cnt * 96 + 32 * plo, staged_key(s, cnt, in, t, plo),
+                      dcodes[d] + plo));
+      uint32_t* po = s->part_out + (size_t)(parts[d].size()) * (OVH_PARTIAL_BYTES / 4);
+      CHK(shard_partial(s, p.slot, (uint32_t)pc, dcodes[d] + plo, po, nullptr));
+      // partial -> devices[0] (peer copy over xGMI), ordered on this device's stream
+      HIPCHK(hipMemcpyPeerAsync(root->gather + k * OVH_PARTIAL_BYTES, s0->device, po, s->device, OVH_PARTIAL_BYTES,
+                                s->stream));
+      parts[d].push_back(p);
+      ++k;
+    }
     HIPCHK(hipEventRecord(s->ev_x[1], s->stream));
-    ++k;
   }
   if (!k) return 0;
   HIPCHK(hipSetDevice(s0->device));
@@ -1951,20 +2028,34 @@ static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
   int32_t verdict = 0;
   HIPCHK(hipMemcpyAsync(&verdict, s0->result + RES_MULTI, 4, hipMemcpyDeviceToHost, s0->fstream));
   HIPCHK(hipStreamSynchronize(s0->fstream));
+  std::vector<std::vector<int32_t>> staged(nd);
   for (size_t d = 0; d < nd; ++d) {
     if (!dcodes[d]) continue;
     ovh_ctx* s = root->sub[d];
     size_t lo, cnt;
     shard_range(n, nd, d, &lo, &cnt);
     HIPCHK(hipSetDevice(s->device));
-    if (!verdict) enqueue_bisect(s, s->stream, slot[d], (uint32_t)cnt, dcodes[d], nullptr);
-    HIPCHK(hipMemcpyAsync(codes + lo, dcodes[d], 4 * cnt, hipMemcpyDeviceToHost, s->stream));
+    if (!verdict)
+      for (const Part& p : parts[d])
+        enqueue_bisect(s, s->stream, p.slot, (uint32_t)p.cnt, dcodes[d] + p.lo, nullptr);
+    int32_t* dst = codes + lo;
+    if (!perms[d].empty()) {
+      staged[d].resize(cnt);
+      dst = staged[d].data();
+    }
+    HIPCHK(hipMemcpyAsync(dst, dcodes[d], 4 * cnt, hipMemcpyDeviceToHost, s->stream));
   }
   for (size_t d = 0; d < nd; ++d)
     if (dcodes[d]) {
       HIPCHK(hipSetDevice(root->sub[d]->device));
       HIPCHK(hipStreamSynchronize(root->sub[d]->stream));
+      if (!perms[d].empty()) {
+        size_t lo, cnt;
+        shard_range(n, nd, d, &lo, &cnt);
+        for (size_t j = 0; j < cnt; ++j) codes[lo + perms[d][j]] = staged[d][j];
+      }
     }
+  HIPCHK(hipSetDevice(root->device));  // the caller's thread back on devices[0]
   return 0;
 }
 
@@ -2016,6 +2107,12 @@ static bool cache_get(ovh_ctx* c, const uint8_t* sig, const uint8_t* hash, const
 }
 
 // ---- key parse
+// a parsed secret scalar on the host stack, wiped when it goes out of scope
+struct SecretBytes {
+  uint8_t b[32];
+  ~SecretBytes() { keygen::wipe(b, sizeof b); }
+};
+
 static int sk_parse(const ovh_ctx* c, const uint8_t* key, size_t len, uint8_t out[32]) {
   const bool ok = (c->flags & OVH_FLAG_SK_RAW) ? keygen::sk_raw(out, key, len) : keygen::key_gen(out, key, len);
   return ok ? 0 : BLST_BAD_ENCODING;
@@ -2045,8 +2142,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking) == hipSuccess &&
-            hipMalloc(&c->part_out, 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
+            hipMalloc(&c->part_out, 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
             hipMalloc(&c->vstart, 8) == hipSuccess && hipMemset(c->vstart, 0, 8) == hipSuccess &&
             hipMemset(c->result, 0, 64) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
@@ -2069,7 +2165,9 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
 }
 
 ovh_ctx* ovh_create_multi(const int* devices, int ndev, const uint8_t* dst, size_t dst_len, uint32_t flags) {
-  if (!devices || ndev < 1 || ndev > 16) return nullptr;
+  // up to 8 devices (one node): two partials per device (table / other votes) fill the 16-entry
+  // gather buffer and one fold level
+  if (!devices || ndev < 1 || ndev > 8) return nullptr;
   ovh_ctx* root = new (std::nothrow) ovh_ctx();
   if (!root) return nullptr;
   root->device = devices[0];
@@ -2247,16 +2345,18 @@ static int enqueue_sign(ovh_ctx* c, size_t n, const uint8_t* d_sks, const uint8_
 int ovh_sign(ovh_ctx* c, const uint8_t* key, size_t key_len, const uint8_t* hash, size_t hash_len, uint8_t out[96]) {
   if (!c || !out) return OVH_ERR_ARG;
   if (hash_len != 32 || !hash) return OVH_ERR_HASH_LEN;
-  uint8_t sk[32];
-  CHK(sk_parse(c, key, key_len, sk));
+  SecretBytes sk;
+  CHK(sk_parse(c, key, key_len, sk.b));
   c = pick_sub(c);
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   CHK(ensure_in(c, 256));
   CHK(ensure_scr(c, 1));
-  HIPCHK(hipMemcpyAsync(c->in_buf, sk, 32, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->in_buf, sk.b, 32, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(c->in_buf + 32, hash, 32, hipMemcpyHostToDevice, c->stream));
   CHK(enqueue_sign(c, 1, c->in_buf, c->in_buf + 32, c->in_buf + 64));
+  // the scalar does not outlive the call: staging bytes zeroed after the kernel, host copy wiped
+  HIPCHK(hipMemsetAsync(c->in_buf, 0, 32, c->stream));
   HIPCHK(hipMemcpyAsync(out, c->in_buf + 64, 96, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
@@ -2264,15 +2364,16 @@ int ovh_sign(ovh_ctx* c, const uint8_t* key, size_t key_len, const uint8_t* hash
 
 int ovh_sk_to_pk(ovh_ctx* c, const uint8_t* key, size_t key_len, uint8_t out[48]) {
   if (!c || !out) return OVH_ERR_ARG;
-  uint8_t sk[32];
-  CHK(sk_parse(c, key, key_len, sk));
+  SecretBytes sk;
+  CHK(sk_parse(c, key, key_len, sk.b));
   c = pick_sub(c);
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   CHK(ensure_in(c, 128));
-  HIPCHK(hipMemcpyAsync(c->in_buf, sk, 32, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->in_buf, sk.b, 32, hipMemcpyHostToDevice, c->stream));
   k_sk_to_pk<<<1, WG, 0, c->stream>>>(1, c->in_buf, c->in_buf + 32);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipMemsetAsync(c->in_buf, 0, 32, c->stream));
   HIPCHK(hipMemcpyAsync(out, c->in_buf + 32, 48, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;
@@ -2282,7 +2383,11 @@ int ovh_verify(ovh_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* ha
                size_t pk_len) {
   if (!c) return OVH_ERR_ARG;
   if (hash_len != 32 || !hash) return OVH_ERR_HASH_LEN;
-  if (sig_len > 4096 || pk_len > 4096 || (sig_len && !sig) || (pk_len && !pk)) return OVH_ERR_ARG;
+  if ((sig_len && !sig) || (pk_len && !pk)) return OVH_ERR_ARG;
+  // consensus.rs:406-410 order: an encoding of any other length never parses; an over-long one
+  // is passed on as empty, so the kernel answers with the reference's precedence (key first: 102)
+  if (pk_len > 4096) pk_len = 0;
+  if (sig_len > 4096) sig_len = 0;
   const bool fixed = sig_len == 96 && pk_len == 48;
   int32_t code;
   if (fixed && cache_get(c, sig, hash, pk, &code)) return code;
@@ -2293,15 +2398,11 @@ int ovh_verify(ovh_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* ha
     // one standalone vote (vote1 / vote_t1 + final1): the vote's own pairing check; a failed
     // check with a clean parse is VERIFY_FAIL (set by k_vm_final1)
     uint8_t* d;
-    CHK(stage_batch(s, 1, sig, hash, pk, &d));
+    size_t t;
+    std::vector<uint32_t> perm;
+    CHK(stage_split(s, 1, sig, hash, pk, &d, &t, perm));
     int32_t* dc = (int32_t*)(d + 176);
-    std::vector<int32_t> idx;
-    KeySrc key{d + 128, PkSrc{}};
-    if (table_lookup(s, 1, pk, idx)) {
-      HIPCHK(hipMemcpyAsync(dc + 1, idx.data(), 4, hipMemcpyHostToDevice, s->stream));
-      key = KeySrc{nullptr, PkSrc{s->tab.planes, s->tab.cap, s->tab.flags, dc + 1}};
-    }
-    CHK(verify_one_locked(s, d, d + 96, key, dc));
+    CHK(verify_one_locked(s, d, d + 96, staged_key(s, 1, d, t, 0), dc));
     int32_t out = -1;
     HIPCHK(hipMemcpyAsync(&out, dc, 4, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
@@ -2379,6 +2480,9 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
   if (n) {
     // the keys parse on the side stream while the signatures run through the VM
     HIPCHK(hipEventRecord(c->ev_x[2], c->stream));  // staged inputs
+    // created on first use: a context that only verifies batches keeps to three streams, which
+    // map onto distinct hardware queues at HIP's default of four (GPU_MAX_HW_QUEUES)
+    if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
     HIPCHK(hipStreamWaitEvent(c->xstream, c->ev_x[2], 0));
     k_parse_pk_list<<<nblk(n), WG, 0, c->xstream>>>((uint32_t)n, dp, po, pl, c->scr_pk, ppts);
     HIPCHK(hipGetLastError());
@@ -2841,7 +2945,10 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   }
   // pipelined: only hash_to_field + the vote kernel on the main stream; the fold levels, the MSM
   // and the packing on the slot's final stream (behind the residency gate), which the caller's
-  // stream then waits for (its all-gather, then ovh_combine_partials_device_async)
+  // stream then waits for (its all-gather, then ovh_combine_partials_device_async). The main
+  // stream first waits for the caller's stream: the inputs may still be in flight there.
+  HIPCHK(hipEventRecord(c->ev_x[0], st));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_x[0], 0));
   CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false));
   hipStream_t fst = c->fs[slot];
   int reg;

@@ -11,7 +11,8 @@
 namespace ovh {
 
 constexpr uint32_t VOTE_HASH_MAX = 64;       // block_hash bytes per vote (stride of the inputs)
-constexpr uint32_t VOTE_RLP_MAX = 2 + 9 + 9 + 1 + 2 + VOTE_HASH_MAX;
+// list header 2, height 9, round 9, vote_type 2 (a type >= 0x80 encodes as 0x81 xx), hash 2 + 64
+constexpr uint32_t VOTE_RLP_MAX = 2 + 9 + 9 + 2 + 2 + VOTE_HASH_MAX;
 
 // an unsigned integer: 0x80 for zero, a single byte < 0x80 as itself, else 0x80 + len || BE
 SM3_HD uint32_t rlp_uint(uint8_t* o, uint64_t v) {

@@ -64,6 +64,7 @@ class ShardVerifier:
         self.rank = dist.get_rank(group)
         self.nccl = dist.get_backend(group) == "nccl"
         self.partials = backend.empty_partials(self.world)   # one per batch in flight (pipelining)
+        self._inflight = []
 
     def _all_gather(self, part: torch.Tensor) -> None:
         mine = part[self.rank].clone()
@@ -78,6 +79,9 @@ class ShardVerifier:
         wait()."""
         part = self.partials[s % self.partials.shape[0]]
         st = getattr(self.backend, "stream", None)
+        # the library's streams read the inputs and write `codes` after this call returns: the
+        # tensors stay referenced until wait(), so the caching allocator cannot hand them out
+        self._inflight.append((sigs, hashes, pks, codes))
         if st is not None:
             st.wait_stream(torch.cuda.current_stream())   # the caller's inputs
             with torch.cuda.stream(st):
@@ -92,6 +96,7 @@ class ShardVerifier:
 
     def wait(self) -> None:
         self.backend.wait()
+        self._inflight.clear()
 
 
 def shard_bounds(n_total: int, world: int, rank: int):

@@ -62,7 +62,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
  * ovh_prefetch split a batch into contiguous shards, one per device; each device computes its
  * shard's 864-byte partial, the partials are copied peer-to-peer (xGMI) to devices[0], which
  * runs the one combined check; on failure every device bisects its own shard. Single-call
- * entry points rotate over the devices. Devices may repeat (tests use {0, 0}). */
+ * entry points rotate over the devices. Devices may repeat (tests use {0, 0}); 1 <= ndev <= 8. */
 ovh_ctx* ovh_create_multi(const int* devices, int ndev, const uint8_t* dst, size_t dst_len, uint32_t flags);
 void ovh_destroy(ovh_ctx* ctx);
 /* Number of devices of the context (1 for ovh_create). */

@@ -139,3 +139,15 @@ def test_check_block_on_device(net):
     assert got == [w for _, _, w in cs], [(n, g) for (n, _, _), g in zip(cs, got)]
     assert cc.check_blocks([args for _, args, _ in cs]).tolist() == got
     assert cc.check_block(*cs[0][1], authority_list=net[0][67:]) is False
+
+
+@pytest.mark.gpu
+def test_check_blocks_without_validator_table(net):
+    """No update_pubkeys (or an empty list): check_blocks answers like check_block -- every
+    block False (no authority list, no voters) -- instead of raising."""
+    import consensus_overlord_amd as coa
+    cc = coa.ConsensusCrypto(bytes.fromhex("98" * 32))
+    cs = cases(net)[:3]
+    assert cc.check_blocks([args for _, args, _ in cs]).tolist() == [False] * 3
+    cc.update_pubkeys([])
+    assert cc.check_blocks([args for _, args, _ in cs]).tolist() == [False] * 3

@@ -154,3 +154,47 @@ def test_qc_batch_matches_verify_aggregated(golden):
     want = [orc.verify_aggregated(s, hh, list(v)) for s, hh, v in qcs]
     assert got.tolist() == want
     assert want[:4] == [0, 5, 5, 4] and want[4] == 102 and want[6] == 0
+
+
+def test_table_split_mixed_batch(golden):
+    """A batch whose voters are partly in the validator table: the table votes run vote_t, the
+    rest the vote program (two combined checks), and every code still equals the oracle's --
+    unknown voters, invalid signatures and keys that do not parse included; the same through a
+    two-device context, whose shards split the same way."""
+    import consensus_overlord_amd as coa
+    from consensus_overlord_amd.crypto import Context
+    c = coa.ConsensusCrypto(bytes.fromhex("99" * 32))
+    n = 300
+    sigs, hs, pks = sv.make(c.ctx, n, lo=70000)
+    for i in range(0, n, 37):
+        sigs[i] = np.frombuffer(sv.add_g2(bytes(sigs[i])), dtype=np.uint8)
+    bad_parse = _b([x for x in golden["verify"] if x["name"] == "pk_x_eq_p"][0]["pk"])
+    pks[5] = np.frombuffer(bad_parse, dtype=np.uint8)     # in the table, does not parse
+    pks[6] = np.frombuffer(bad_parse, dtype=np.uint8)
+    table = [bytes(pks[i]) for i in range(0, n, 2)] + [bad_parse]
+    c.update_pubkeys(table)
+    want = sv.oracle_codes(sigs, hs, pks)
+    args = (list(map(bytes, sigs)), list(map(bytes, hs)), list(map(bytes, pks)))
+    assert c.verify_batch(*args).tolist() == want.tolist()
+    multi = coa.ConsensusCrypto(bytes.fromhex("99" * 32), ctx=Context(devices=[0, 0]))
+    multi.update_pubkeys(table)
+    assert multi.verify_batch(*args).tolist() == want.tolist()
+    # per call: a table voter and an unknown voter
+    for i in (1, 2, 37, 74):
+        assert c.lib.ovh_verify(c.ctx.ptr, bytes(sigs[i]), 96, bytes(hs[i]), 32, bytes(pks[i]), 48) == want[i]
+
+
+def test_oversized_encodings_keep_reference_precedence(golden):
+    """consensus.rs:403-414 order for encodings of any length: hash length, then the key parse
+    (102), then the signature parse (BAD_ENCODING) -- also past the staging limit."""
+    import consensus_overlord_amd as coa
+    c = coa.ConsensusCrypto(bytes.fromhex("aa" * 32))
+    v = [x for x in golden["verify"] if x["name"].startswith("valid_")][0]
+    s, h, p = _b(v["sig"]), _b(v["hash"]), _b(v["pk"])
+    big = bytes(5000)
+    L = c.lib
+    assert L.ovh_verify(c.ctx.ptr, s, 96, h, 32, p, 48) == 0
+    assert L.ovh_verify(c.ctx.ptr, s, 96, h, 32, big, len(big)) == 102
+    assert L.ovh_verify(c.ctx.ptr, big, len(big), h, 32, p, 48) == 1
+    assert L.ovh_verify(c.ctx.ptr, big, len(big), h, 32, big, len(big)) == 102
+    assert L.ovh_verify(c.ctx.ptr, big, len(big), h, 31, big, len(big)) == 100

@@ -27,6 +27,9 @@ def edge_votes():
             out.append((h, r, vote.PREVOTE if (h + r) % 2 else vote.PRECOMMIT, bytes(32)))
     for ln in (0, 1, 2, 31, 32, 33, 54, 55, 56, 63, 64):
         out.append((7, 3, vote.PRECOMMIT, bytes(rng.randrange(256) for _ in range(ln))))
+    # vote types >= 0x80 encode as two bytes (0x81 xx): the longest RLP, 88 bytes
+    for t in (0x7F, 0x80, 0xFF):
+        out.append((2 ** 64 - 1, 2 ** 64 - 1, t, bytes(rng.randrange(256) for _ in range(64))))
     out.append((9, 2, vote.PREVOTE, b"\x00"))
     out.append((9, 2, vote.PREVOTE, b"\x7f"))
     out.append((9, 2, vote.PREVOTE, b"\x80"))
@@ -66,3 +69,33 @@ def test_device_vote_digests():
     votes = edge_votes()
     assert cc.vote_digests(votes) == [want(v) for v in votes]
     assert cc.vote_digests([APPX_B])[0].hex() == APPX_B_SM3
+
+
+@pytest.mark.gpu
+def test_device_vote_digest_rejects_overlong_hash():
+    """ovh_vote_digests_device reads the lengths from device memory: a length above 64 gets the
+    all-zero digest instead of overrunning the kernel's 64-byte hash buffer."""
+    import torch
+    import consensus_overlord_amd as coa
+    from consensus_overlord_amd.crypto import Context
+    ctx = Context(0)
+    votes = [(5, 1, vote.PRECOMMIT, bytes(range(64))), (5, 1, vote.PRECOMMIT, bytes(range(64))), APPX_B]
+    lens = [64, 200, len(APPX_B[3])]
+    n = len(votes)
+    h = torch.tensor([v[0] for v in votes], dtype=torch.int64).cuda()
+    r = torch.tensor([v[1] for v in votes], dtype=torch.int64).cuda()
+    t = torch.tensor([v[2] for v in votes], dtype=torch.uint8).cuda()
+    bh = torch.zeros((n, 64), dtype=torch.uint8)
+    for i, v in enumerate(votes):
+        bh[i, :len(v[3])] = torch.tensor(list(v[3]), dtype=torch.uint8)
+    bh = bh.cuda()
+    ln = torch.tensor(lens, dtype=torch.uint8).cuda()
+    out = torch.full((n, 32), 0xAA, dtype=torch.uint8).cuda()
+    p = lambda x: ctypes.c_void_p(x.data_ptr())   # noqa: E731
+    coa.crypto.raise_for(ctx.lib.ovh_vote_digests_device(ctx.ptr, n, p(h), p(r), p(t), p(bh), p(ln), p(out)))
+    torch.cuda.synchronize()
+    got = [bytes(out[i].cpu().numpy()) for i in range(n)]
+    assert got[0] == want(votes[0])
+    assert got[1] == bytes(32)
+    assert got[2].hex() == APPX_B_SM3
+    ctx.close()
