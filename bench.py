@@ -223,6 +223,49 @@ def latencies(ctx, sigs, hs, pks) -> dict:
     return out
 
 
+def multi_device_leg(args) -> None:
+    """One process over several GPUs through the C ABI alone (ovh_create_multi +
+    ovh_verify_batch_async + ovh_batch_wait): what a node linking libovhip.so without torch
+    runs. Host buffers: the timed region includes staging into pinned memory and the PCIe copies
+    (176 B in, 4 B out per vote); each step is one batch of --batch votes per device."""
+    import torch
+    from consensus_overlord_amd import device as dev
+    from consensus_overlord_amd.crypto import ConsensusCrypto, Context
+    devs = list(range(torch.cuda.device_count())) if args.multi_device == "all" else \
+        [int(x) for x in args.multi_device.split(",")]
+    one = Context(devs[0])
+    n = args.batch * len(devs)
+    sks_h, hs_h = synth_inputs(one.lib, 0, n)
+    sks = torch.from_numpy(sks_h).cuda()
+    hs = torch.from_numpy(hs_h).cuda()
+    pks = dev.sk_to_pk_batch(one, sks).cpu().numpy()
+    sigs = dev.sign_batch(one, sks, hs).cpu().numpy()
+    one.close()
+    c = ConsensusCrypto(bytes(31) + b"\x01", ctx=Context(devices=devs))
+    S, H, P = list(map(bytes, sigs)), list(map(bytes, hs_h)), list(map(bytes, pks))
+    outs = [np.full(n, -1, dtype=np.int32) for _ in range(args.warmup + args.steps)]
+    for s in range(args.warmup):
+        c.verify_batch_async(S, H, P, outs[s])
+    c.wait()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        c.verify_batch_async(S, H, P, outs[args.warmup + s])
+    c.wait()
+    elapsed = time.perf_counter() - t0
+    if any((o != 0).any() for o in outs):
+        raise RuntimeError("multi-device batches rejected valid votes")
+    print(json.dumps({
+        "metric": "BLS12-381 vote verifications/sec (batch 4096) at 1/2/4/8 MI355X vs host blst",
+        "value": round(n * args.steps / elapsed, 2), "unit": "verifications/s", "n_gpus": len(set(devs)),
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (seed 0xC17A keypairs + RLP precommit votes, SURVEY.md 8(d))",
+        "config": {"workload": "config3 votes, %d per device per batch, host buffers" % args.batch,
+                   "devices": devs, "parallelism": "one process, ovh_create_multi over %d device pipelines, "
+                   "partials peer-copied to a rotating final device" % len(devs)},
+        "note": "multi-device leg: includes host staging + PCIe copies; not the driver's metric line"}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -237,8 +280,14 @@ def main():
     ap.add_argument("--no-latency", action="store_true", help="skip the untimed latency probes")
     ap.add_argument("--shard-path", action="store_true",
                     help="diagnostic: run the multi-GPU pipeline (partials + RCCL all-gather) even at N=1")
+    ap.add_argument("--multi-device", default=None, metavar="DEVS",
+                    help="the one-process multi-GPU path a Rust node uses: ovh_create_multi over DEVS "
+                         "('all' = every visible GPU, or e.g. '0,0'), host-buffer batches of --batch votes "
+                         "per device pipelined through ovh_verify_batch_async")
     args = ap.parse_args()
 
+    if args.multi_device:
+        return multi_device_leg(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -247,6 +247,21 @@ class ConsensusCrypto:
         raise_for(self.lib.ovh_verify_batch(self.ctx.ptr, n, sig, hs, pk, codes.ctypes.data_as(ctypes.c_void_p)))
         return codes[:n]
 
+    def verify_batch_async(self, signatures, hashes, voters, codes: np.ndarray) -> None:
+        """Pipelined verify_batch (ovh_verify_batch_async, any context kind): returns at once;
+        `codes` (int32[n], kept alive by this object until wait) is final after wait()."""
+        n, sig, hs, pk = self._fixed(signatures, hashes, voters)
+        if codes.dtype != np.int32 or codes.shape != (n,) or not codes.flags.c_contiguous:
+            raise ValueError("codes must be a contiguous int32[n] array")
+        self._inflight = getattr(self, "_inflight", [])
+        self._inflight.append(codes)
+        raise_for(self.lib.ovh_verify_batch_async(self.ctx.ptr, n, sig, hs, pk, codes.ctypes.data_as(ctypes.c_void_p)))
+
+    def wait(self) -> None:
+        """ovh_batch_wait: every batch in flight is complete, its codes written."""
+        raise_for(self.lib.ovh_batch_wait(self.ctx.ptr))
+        self._inflight = []
+
     def prefetch(self, signatures, hashes, voters) -> None:
         """Vote-batching ingress (ovh_prefetch): batch-verify the votes now; later
         verify_signature calls on the same bytes are answered from the context's cache."""

@@ -1228,6 +1228,19 @@ struct VerdictCache {
   uint64_t hits = 0, misses = 0;
 };
 
+// A pipelined host-buffer batch in flight (ovh_verify_batch_async): per device its shard, the
+// staging order (table_split perm) and the ring slot whose pinned buffer receives its codes.
+struct HostBatch {
+  int32_t* codes = nullptr;  // the caller's, written when the batch completes
+  size_t n = 0;
+  int ring = 0;
+  struct Dev {
+    size_t d, lo, cnt;
+    std::vector<uint32_t> perm;
+  };
+  std::vector<Dev> dev;
+};
+
 struct ovh_ctx {
   int device = 0;
   uint32_t flags = 0;
@@ -1263,7 +1276,7 @@ struct ovh_ctx {
   uint32_t scr_cap = 0;
   uint32_t* comb = nullptr;  // ovh_combine_partials_device scratch
   uint32_t comb_cap = 0;
-  uint32_t* part_out = nullptr;  // multi-device: this device's partials (2 x 216 words: table / other votes)
+  uint32_t* part_out = nullptr;  // multi-device: this device's partials (ring slot x {table, other votes} x 216 words)
   int32_t* result = nullptr;     // device verdict words
   unsigned long long* vstart = nullptr;  // vote workgroups started (k_gate), device
   uint64_t vlaunched = 0;                // vote workgroups launched, host
@@ -1286,6 +1299,17 @@ struct ovh_ctx {
   // entries, bucket trees, bit-plane sums) and the slot's RLC seed (the bisection's k_vm_rs)
   uint32_t* msm_buf[OVH_BATCH_SLOTS] = {};
   uint64_t slot_seed[OVH_BATCH_SLOTS] = {}, slot_base[OVH_BATCH_SLOTS] = {};
+  // pipelined host batches (ovh_verify_batch_async): per ring slot a pinned host staging buffer
+  // (inputs, then the codes read back) and its device copy; events per ring slot: [0], [1] the
+  // packed partials of the slot's two parts, [2] the combined verdict (final device), [3] the codes
+  // in the pinned buffer
+  uint8_t* hst_h[OVH_BATCH_SLOTS] = {};
+  uint8_t* hst_d[OVH_BATCH_SLOTS] = {};
+  size_t hst_cap[OVH_BATCH_SLOTS] = {};
+  hipEvent_t ev_m[OVH_BATCH_SLOTS][4] = {};
+  uint8_t* mg = nullptr;  // as a multi context's final device: OVH_BATCH_SLOTS x 16 gathered partials
+  std::deque<HostBatch> hq;  // batches in flight (the root context / a single context)
+  uint64_t hb_k = 0;
   // Fp-VM programs + constant table in device memory
   VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{},
       vm_pkchk{}, vm_g1padd{}, vm_sign0{}, vm_sign1{}, vm_vote1{}, vm_vote_t1{}, vm_final1{};
@@ -1669,7 +1693,8 @@ static int fold_down(ovh_ctx* c, int slot, hipStream_t st, int slices, int* reg,
 // Verdict words in c->result: [0] single calls, then per slot the batch verdicts, the combine
 // verdicts, then the synchronous combine's and the multi-device combine's.
 enum { RES_BATCH = 4, RES_COMBINE = RES_BATCH + OVH_BATCH_SLOTS, RES_SYNC = RES_COMBINE + OVH_BATCH_SLOTS, RES_MULTI };
-static_assert(RES_MULTI < 16, "verdict words fit c->result");
+// RES_MULTI: the synchronous multi-device verdict; RES_MULTI + 1 + ring slot: the pipelined ones
+static_assert(RES_MULTI + 1 + OVH_BATCH_SLOTS <= 16, "verdict words fit c->result");
 
 // Final check on <= 4 partials given as planes: k_vm_final on stream `st`, verdict to *d_res;
 // xS: the batch's MSM result (partial 0's S), or {nullptr} when the partials carry their S.
@@ -1959,6 +1984,8 @@ static void shard_range(size_t n, size_t nd, size_t d, size_t* lo, size_t* cnt) 
   *cnt = base + (d < extra ? 1 : 0);
 }
 
+static int drain_host(ovh_ctx* root);
+
 static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
                              int32_t* codes) {
   const size_t nd = root->sub.size();
@@ -1966,6 +1993,7 @@ static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
   locks.emplace_back(root->mu);
   for (ovh_ctx* s : root->sub) locks.emplace_back(s->mu);
   ovh_ctx* s0 = root->sub[0];
+  CHK(drain_host(root));  // pipelined batches first (they share the partial buffers)
   // per device: its shard, staged table-first (stage_split), as up to two parts (table votes,
   // other votes), each a batch with its own partial
   struct Part {
@@ -2059,6 +2087,215 @@ static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
   return 0;
 }
 
+static int stage_partials(ovh_ctx* c, hipStream_t st, size_t k, const uint8_t* d_partials, uint32_t* scratch, Slab* F,
+                          Slab* S, uint32_t* m);
+
+// ---- pipelined host batches (ovh_verify_batch_async) on single and multi-device contexts
+static std::vector<ovh_ctx*> devices_of(ovh_ctx* c) {
+  return c->sub.empty() ? std::vector<ovh_ctx*>{c} : c->sub;
+}
+
+// pinned host staging + its device copy for ring slot j (>= bytes)
+static int ensure_hst(ovh_ctx* c, int j, size_t bytes) {
+  if (bytes <= c->hst_cap[j] && c->hst_h[j]) return 0;
+  size_t cap = 1 << 16;
+  while (cap < bytes) cap <<= 1;
+  CHK(sync_all(c));
+  if (c->hst_h[j]) (void)hipHostFree(c->hst_h[j]);
+  if (c->hst_d[j]) (void)hipFree(c->hst_d[j]);
+  c->hst_h[j] = nullptr;
+  c->hst_d[j] = nullptr;
+  c->hst_cap[j] = 0;
+  HIPCHK(hipHostMalloc((void**)&c->hst_h[j], cap, hipHostMallocDefault));
+  HIPCHK(hipMalloc(&c->hst_d[j], cap));
+  c->hst_cap[j] = cap;
+  return 0;
+}
+
+// Stage one device's votes for ring slot j: table-first into the pinned buffer, then one H2D copy
+// on the main stream (layout of stage_split: sigs | hashes | pks | codes | table indices).
+static int stage_pinned(ovh_ctx* s, int j, size_t cnt, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                        size_t* t, std::vector<uint32_t>& perm) {
+  std::vector<int32_t> idx;
+  *t = table_split(s, cnt, pks, perm, idx);
+  CHK(ensure_hst(s, j, cnt * 184 + 64));
+  uint8_t* h = s->hst_h[j];
+  if (perm.empty()) {
+    memcpy(h, sigs, cnt * 96);
+    memcpy(h + cnt * 96, hashes, cnt * 32);
+    memcpy(h + cnt * 128, pks, cnt * 48);
+  } else {
+    for (size_t q = 0; q < cnt; ++q) {
+      const size_t i = perm[q];
+      memcpy(h + 96 * q, sigs + 96 * i, 96);
+      memcpy(h + cnt * 96 + 32 * q, hashes + 32 * i, 32);
+      memcpy(h + cnt * 128 + 48 * q, pks + 48 * i, 48);
+    }
+  }
+  if (*t) memcpy(h + cnt * 180, idx.data(), *t * 4);
+  HIPCHK(hipMemcpyAsync(s->hst_d[j], h, cnt * 176, hipMemcpyHostToDevice, s->stream));
+  if (*t) HIPCHK(hipMemcpyAsync(s->hst_d[j] + cnt * 180, h + cnt * 180, *t * 4, hipMemcpyHostToDevice, s->stream));
+  return 0;
+}
+
+// Oldest batch in flight: wait for its codes (pinned) and write them to the caller's array.
+static int complete_front(ovh_ctx* root) {
+  const std::vector<ovh_ctx*> devs = devices_of(root);
+  HostBatch& hb = root->hq.front();
+  for (const HostBatch::Dev& dv : hb.dev) {
+    ovh_ctx* s = devs[dv.d];
+    HIPCHK(hipSetDevice(s->device));
+    HIPCHK(hipEventSynchronize(s->ev_m[hb.ring][3]));
+    const int32_t* pc = (const int32_t*)(s->hst_h[hb.ring] + dv.cnt * 176);
+    if (dv.perm.empty()) memcpy(hb.codes + dv.lo, pc, dv.cnt * 4);
+    else
+      for (size_t q = 0; q < dv.cnt; ++q) hb.codes[dv.lo + dv.perm[q]] = pc[q];
+  }
+  root->hq.pop_front();
+  return 0;
+}
+
+static int drain_host(ovh_ctx* root) {
+  while (!root->hq.empty()) CHK(complete_front(root));
+  return 0;
+}
+
+// One context: the batch's parts (table votes, other votes) through the pipelined batch path
+// (verify_async_locked), the codes read back on the last part's final stream. Caller holds c->mu.
+static int submit_host_single(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                              int32_t* codes) {
+  if (c->hq.size() >= OVH_BATCH_SLOTS) CHK(complete_front(c));
+  const int j = (int)(c->hb_k++ % OVH_BATCH_SLOTS);
+  HostBatch hb;
+  hb.codes = codes;
+  hb.n = n;
+  hb.ring = j;
+  hb.dev.push_back(HostBatch::Dev{0, 0, n, {}});
+  size_t t;
+  CHK(stage_pinned(c, j, n, sigs, hashes, pks, &t, hb.dev[0].perm));
+  uint8_t* in = c->hst_d[j];
+  int32_t* dc = (int32_t*)(in + n * 176);
+  hipStream_t last = c->stream;
+  if (n == 1) {
+    CHK(verify_one_locked(c, in, in + 96, staged_key(c, n, in, t, 0), dc));
+  } else {
+    int prev = -1;
+    for (size_t lo : {(size_t)0, t}) {
+      const size_t cnt = lo == 0 ? t : n - t;
+      if (!cnt) continue;
+      CHK(verify_async_locked(c, cnt, in + 96 * lo, in + n * 96 + 32 * lo, staged_key(c, n, in, t, lo), dc + lo, true));
+      if (prev >= 0) HIPCHK(hipStreamWaitEvent(c->fs[c->last_slot], c->ev_back[prev], 0));
+      prev = c->last_slot;
+      last = c->fs[c->last_slot];
+    }
+  }
+  HIPCHK(hipMemcpyAsync(c->hst_h[j] + n * 176, dc, n * 4, hipMemcpyDeviceToHost, last));
+  HIPCHK(hipEventRecord(c->ev_m[j][3], last));
+  c->hq.push_back(std::move(hb));
+  return 0;
+}
+
+// Several devices: per device its shard's parts through hash_to_field + the vote kernel (main
+// stream) and the fold levels, MSM and packing (final stream), each packed partial peer-copied
+// to this batch's final device -- devices[k mod ndev] for the k-th batch, so the combined checks
+// rotate -- whose final stream runs the combined check and sends the verdict back to every
+// device; each device then runs its device-gated bisection and reads its codes back. Nothing
+// blocks the host: the next batch's per-vote work overlaps this batch's combined check on every
+// device. Caller holds root->mu and every device's mu.
+static int submit_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                             int32_t* codes) {
+  const size_t nd = root->sub.size();
+  if (root->hq.size() >= OVH_BATCH_SLOTS) CHK(complete_front(root));
+  const int j = (int)(root->hb_k % OVH_BATCH_SLOTS);
+  ovh_ctx* F = root->sub[root->hb_k % nd];
+  ++root->hb_k;
+  HostBatch hb;
+  hb.codes = codes;
+  hb.n = n;
+  hb.ring = j;
+  struct Part {
+    ovh_ctx* s;
+    int slot, pi;
+    size_t plo, pc;
+    int32_t* dcodes;
+  };
+  std::vector<Part> ps;
+  std::vector<size_t> first;  // index into ps of each device's first part
+  size_t k = 0;
+  if (!F->mg) {
+    HIPCHK(hipSetDevice(F->device));
+    HIPCHK(hipMalloc(&F->mg, (size_t)OVH_BATCH_SLOTS * 16 * OVH_PARTIAL_BYTES));
+  }
+  uint8_t* gather = F->mg + (size_t)j * 16 * OVH_PARTIAL_BYTES;
+  for (size_t d = 0; d < nd; ++d) {
+    ovh_ctx* s = root->sub[d];
+    size_t lo, cnt;
+    shard_range(n, nd, d, &lo, &cnt);
+    if (!cnt) continue;
+    HIPCHK(hipSetDevice(s->device));
+    hb.dev.push_back(HostBatch::Dev{d, lo, cnt, {}});
+    size_t t;
+    CHK(stage_pinned(s, j, cnt, sigs + lo * 96, hashes + lo * 32, pks + lo * 48, &t, hb.dev.back().perm));
+    uint8_t* in = s->hst_d[j];
+    int32_t* dcodes = (int32_t*)(in + cnt * 176);
+    CHK(ensure_cap(s, cnt));
+    first.push_back(ps.size());
+    int pi = 0;
+    for (size_t plo : {(size_t)0, t}) {
+      const size_t pc = plo == 0 ? t : cnt - t;
+      if (!pc) continue;
+      int slot;
+      CHK(take_slot(s, &slot));
+      s->test_base = root->test_base + lo + plo;  // OVH_FLAG_TEST_RLC only: one global index per vote
+      CHK(batch_front(s, slot, (uint32_t)pc, in + 96 * plo, in + cnt * 96 + 32 * plo, staged_key(s, cnt, in, t, plo),
+                      dcodes + plo, false));
+      const hipStream_t fst = s->fs[slot];
+      int reg;
+      uint32_t m;
+      CHK(side_front(s, slot, (uint32_t)pc, true, 1, &reg, &m));
+      CHK(enqueue_msm(s, fst, slot, (uint32_t)pc, dcodes + plo));
+      uint32_t* po = s->part_out + ((size_t)j * 2 + pi) * (OVH_PARTIAL_BYTES / 4);
+      k_pack_partial2<<<1, 64, 0, fst>>>(region_F(s, slot, reg), msm_S(s, slot), po);
+      HIPCHK(hipMemcpyPeerAsync(gather + k * OVH_PARTIAL_BYTES, F->device, po, s->device, OVH_PARTIAL_BYTES, fst));
+      HIPCHK(hipEventRecord(s->ev_m[j][pi], fst));
+      ps.push_back(Part{s, slot, pi, plo, pc, dcodes});
+      ++k;
+      ++pi;
+    }
+  }
+  // the combined check on the batch's final device
+  HIPCHK(hipSetDevice(F->device));
+  for (const Part& p : ps) HIPCHK(hipStreamWaitEvent(F->fstream, p.s->ev_m[j][p.pi], 0));
+  Slab PF, PS;
+  uint32_t m;
+  CHK(stage_partials(F, F->fstream, k, gather, F->fin + (size_t)j * FIN_STRIDE, &PF, &PS, &m));
+  int32_t* fv = F->result + RES_MULTI + 1 + j;
+  enqueue_final(F, F->fstream, PF, PS, m, fv);
+  for (size_t q : first)
+    if (ps[q].s != F)
+      HIPCHK(hipMemcpyPeerAsync(ps[q].s->result + RES_MULTI + 1 + j, ps[q].s->device, fv, F->device, 4, F->fstream));
+  HIPCHK(hipEventRecord(F->ev_m[j][2], F->fstream));
+  // per device: device-gated bisection of its parts, then the codes into the pinned buffer
+  for (size_t e = 0; e < first.size(); ++e) {
+    const Part& p0 = ps[first[e]];
+    ovh_ctx* s = p0.s;
+    const size_t end = e + 1 < first.size() ? first[e + 1] : ps.size();
+    const size_t cnt = hb.dev[e].cnt;
+    HIPCHK(hipSetDevice(s->device));
+    const hipStream_t bst = s->fs[p0.slot];
+    HIPCHK(hipStreamWaitEvent(bst, F->ev_m[j][2], 0));
+    for (size_t q = first[e]; q < end; ++q) {
+      enqueue_bisect(s, bst, ps[q].slot, (uint32_t)ps[q].pc, ps[q].dcodes + ps[q].plo, s->result + RES_MULTI + 1 + j);
+      HIPCHK(hipEventRecord(s->ev_back[ps[q].slot], bst));
+    }
+    HIPCHK(hipMemcpyAsync(s->hst_h[j] + cnt * 176, p0.dcodes, cnt * 4, hipMemcpyDeviceToHost, bst));
+    HIPCHK(hipEventRecord(s->ev_m[j][3], bst));
+  }
+  HIPCHK(hipGetLastError());
+  root->hq.push_back(std::move(hb));
+  return 0;
+}
+
 static ovh_ctx* pick_sub(ovh_ctx* c) {
   if (c->sub.empty()) return c;
   return c->sub[c->rr.fetch_add(1) % c->sub.size()];
@@ -2142,7 +2379,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipMalloc(&c->part_out, 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
+            hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
             hipMalloc(&c->vstart, 8) == hipSuccess && hipMemset(c->vstart, 0, 8) == hipSuccess &&
             hipMemset(c->result, 0, 64) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
@@ -2154,6 +2391,8 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
     ok = hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_back[k], hipEventDisableTiming) == hipSuccess;
   for (int k = 0; ok && k < 4; ++k) ok = hipEventCreateWithFlags(&c->ev_x[k], hipEventDisableTiming) == hipSuccess;
+  for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k)
+    for (int q = 0; ok && q < 4; ++q) ok = hipEventCreateWithFlags(&c->ev_m[k][q], hipEventDisableTiming) == hipSuccess;
   if (ok && (flags & OVH_FLAG_PROFILE))
     for (int k = 0; ok && k < OVH_NSTAGES; ++k)
       ok = hipEventCreate(&c->ev0[k]) == hipSuccess && hipEventCreate(&c->ev1[k]) == hipSuccess;
@@ -2215,6 +2454,13 @@ static void destroy_one(ovh_ctx* c) {
       if (e) (void)hipEventDestroy(e);
   for (int k = 0; k < 4; ++k)
     if (c->ev_x[k]) (void)hipEventDestroy(c->ev_x[k]);
+  for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
+    for (int q = 0; q < 4; ++q)
+      if (c->ev_m[k][q]) (void)hipEventDestroy(c->ev_m[k][q]);
+    if (c->hst_h[k]) (void)hipHostFree(c->hst_h[k]);
+    if (c->hst_d[k]) (void)hipFree(c->hst_d[k]);
+  }
+  if (c->mg) (void)hipFree(c->mg);
   for (int k = 0; k < OVH_NSTAGES; ++k) {
     if (c->ev0[k]) (void)hipEventDestroy(c->ev0[k]);
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
@@ -2897,11 +3143,47 @@ int ovh_verify_batch_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, c
   return verify_async_locked(c, n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, true);
 }
 
+// every device's lock, root first (the multi-device entry points)
+static std::vector<std::unique_lock<std::mutex>> lock_all(ovh_ctx* c) {
+  std::vector<std::unique_lock<std::mutex>> locks;
+  locks.emplace_back(c->mu);
+  for (ovh_ctx* s : c->sub) locks.emplace_back(s->mu);
+  return locks;
+}
+
+// restores the caller thread's current HIP device when it goes out of scope
+struct DeviceGuard {
+  int dev = -1;
+  DeviceGuard() { (void)hipGetDevice(&dev); }
+  ~DeviceGuard() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+};
+
+int ovh_verify_batch_async(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                           int32_t* codes) {
+  if (!c || (n && (!sigs || !hashes || !pks || !codes))) return OVH_ERR_ARG;
+  if (n == 0) return 0;
+  if (n > (1u << 24)) return OVH_ERR_ARG;
+  DeviceGuard dg;
+  auto locks = lock_all(c);
+  if (c->sub.empty()) {
+    HIPCHK(hipSetDevice(c->device));
+    return submit_host_single(c, n, sigs, hashes, pks, codes);
+  }
+  return submit_host_multi(c, n, sigs, hashes, pks, codes);
+}
+
 int ovh_batch_wait(ovh_ctx* c) {
-  if (!c || !c->sub.empty()) return OVH_ERR_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  HIPCHK(hipSetDevice(c->device));
-  return sync_all(c);
+  if (!c) return OVH_ERR_ARG;
+  DeviceGuard dg;
+  auto locks = lock_all(c);
+  CHK(drain_host(c));
+  for (ovh_ctx* s : devices_of(c)) {
+    HIPCHK(hipSetDevice(s->device));
+    CHK(sync_all(s));
+  }
+  return 0;
 }
 
 int ovh_verify_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, const uint8_t* d_pks,

@@ -190,6 +190,18 @@ int ovh_batch_fallback_device(ovh_ctx* ctx, size_t n, int32_t* d_codes);
 #define OVH_BATCH_SLOTS 3 /* batches in flight per context (state slots) */
 int ovh_verify_batch_device_async(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
                                   const uint8_t* d_pks, int32_t* d_codes);
+/* The pipelined form with host buffers, for single- and multi-device contexts (a node with no
+ * torch; ovh_create_multi is its multi-GPU path): the inputs are copied into pinned staging
+ * before the call returns (the caller may reuse them at once); `codes` (host, n entries) must
+ * stay valid and is written by a later call of this function or ovh_batch_wait. Per batch each
+ * device runs its shard's per-vote stages on its own pipeline, the partials go peer-to-peer
+ * (xGMI) to the batch's final device, which rotates over the devices batch by batch, and each
+ * device bisects its own shard when the combined check fails. At most OVH_BATCH_SLOTS batches
+ * are in flight: a further call first completes the oldest. The caller's current HIP device is
+ * unchanged on return. */
+int ovh_verify_batch_async(ovh_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
+                           int32_t* codes);
+/* Completes every batch in flight on the context (device or host form, any context kind). */
 int ovh_batch_wait(ovh_ctx* ctx);
 /* Multi-GPU form: after ovh_batch_partial_device (n votes of this rank) and the all-gather of
  * the k <= 16 partials on `stream`, enqueue (stream-ordered after the gather) the combined check
