@@ -16,7 +16,7 @@ import pytest
 
 import synth_votes as sv
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(300)]
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N, SHARDS = 65536, 8
