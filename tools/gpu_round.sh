@@ -7,6 +7,7 @@ R=$(pwd)
 OUT=$R/gpurun_out/${TAG:-r01}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+if [ -x tools/ubench/fp_mul28 ]; then timeout -k 10 60 tools/ubench/fp_mul28 > "$OUT/fp_mul28.log" 2>&1; fi
 timeout -k 10 300 python -c "import torch; print(torch.__version__, torch.cuda.is_available())" > "$OUT/torch.log" 2>&1
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
