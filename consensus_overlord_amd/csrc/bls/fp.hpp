@@ -199,7 +199,205 @@ OVH_HDNI void fp_pow(Fp& r, const Fp& a, const uint32_t* e) {
   r = acc;
 }
 
-OVH_HD void fp_inv(Fp& r, const Fp& a) { fp_pow(r, a, EXP_P_MINUS_2); }
+// Modular inverse of a canonical Montgomery value, then back to Montgomery form with one product
+// by raw R^3 (r3). 0 -> 0. Used by fp_inv (every one-lane kernel) and the Fp-VM's inv op.
+// Bernstein-Yang divsteps, variable time (the inverted value is public batch data): batches of
+// 30 divsteps on the low limbs give a 2x2 transition matrix, applied to (f, g) exactly and to
+// (d, e) modulo p (plus the multiple of p that makes the division by 2^30 exact). Values in 13
+// signed 30-bit limbs (limbs 0..11 in [0, 2^30), limb 12 signed). Invariants: f = d x, g = e x
+// (mod p); f starts at p, g at x; when g reaches 0, f = +-1 and x^-1 = +-d.
+namespace inv {
+constexpr int NL = 13;
+constexpr int32_t M30 = 0x3FFFFFFF;
+constexpr int32_t PL[NL] = {0x3fffaaab, 0x27fbffff, 0x153ffffb, 0x2affffac, 0x30f6241e, 0x034a83da, 0x112bf673,
+                            0x12e13ce1, 0x2cd76477, 0x1ed90d2e, 0x29a4b1ba, 0x3a8e5ff9, 0x001a0111};
+constexpr uint32_t PINV30 = 0x30003;  // p^-1 mod 2^30
+struct Trans {
+  int32_t u, v, q, r;
+};
+
+OVH_HD int ctz32(uint32_t x) { return __builtin_ctz(x); }
+
+// -(f^-1) mod 2^32, f odd (Newton: 3 -> 6 -> 12 -> 24 -> 48 correct bits)
+OVH_HD uint32_t neg_inv32(uint32_t f) {
+  uint32_t x = f;
+  x *= 2u - f * x;
+  x *= 2u - f * x;
+  x *= 2u - f * x;
+  x *= 2u - f * x;
+  return 0u - x;
+}
+
+// 30 divsteps on the low bits of f and g (eta = -delta); t: 2^30 [f', g'] = t [f, g]
+OVH_HD int32_t divsteps30(int32_t eta, uint32_t f, uint32_t g, Trans& t) {
+  uint32_t u = 1, v = 0, q = 0, r = 1, finv = neg_inv32(f);
+  int i = 30;
+#pragma unroll 1
+  for (;;) {
+    // zero low bits of g: halvings (the f row doubles instead), at most i of them
+    const int z = ctz32(g | (0xFFFFFFFFu << i));
+    g >>= z;
+    u <<= z;
+    v <<= z;
+    eta -= z;
+    i -= z;
+    if (i == 0) break;
+    if (eta < 0) {  // swap: (f, g) = (g, -f)
+      eta = -eta;
+      uint32_t x = f;
+      f = g;
+      g = 0u - x;
+      x = u;
+      u = q;
+      q = 0u - x;
+      x = v;
+      v = r;
+      r = 0u - x;
+      finv = neg_inv32(f);
+    }
+    // cancel up to min(eta + 1, i) low bits of g with a multiple of f
+    const int limit = (eta + 1) > i ? i : (eta + 1);
+    const uint32_t w = (g * finv) & (0xFFFFFFFFu >> (32 - limit));
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t.u = (int32_t)u;
+  t.v = (int32_t)v;
+  t.q = (int32_t)q;
+  t.r = (int32_t)r;
+  return eta;
+}
+
+// (f, g) = t (f, g) / 2^30 (exact)
+OVH_HD void update_fg(int32_t* f, int32_t* g, const Trans& t) {
+  const int64_t u = t.u, v = t.v, q = t.q, r = t.r;
+  int64_t cf = u * f[0] + v * g[0], cg = q * f[0] + r * g[0];
+  cf >>= 30;
+  cg >>= 30;
+#pragma unroll
+  for (int i = 1; i < NL; ++i) {
+    cf += u * f[i] + v * g[i];
+    cg += q * f[i] + r * g[i];
+    f[i - 1] = (int32_t)cf & M30;
+    cf >>= 30;
+    g[i - 1] = (int32_t)cg & M30;
+    cg >>= 30;
+  }
+  f[NL - 1] = (int32_t)cf;
+  g[NL - 1] = (int32_t)cg;
+}
+
+// (d, e) = (t (d, e) + p (md, me)) / 2^30, md / me making the division exact and keeping
+// d, e in (-2p, p)
+OVH_HD void update_de(int32_t* d, int32_t* e, const Trans& t) {
+  const int32_t sd = d[NL - 1] >> 31, se = e[NL - 1] >> 31;
+  int32_t md = (t.u & sd) + (t.v & se), me = (t.q & sd) + (t.r & se);
+  const int64_t u = t.u, v = t.v, q = t.q, r = t.r;
+  int64_t cd = u * d[0] + v * e[0], ce = q * d[0] + r * e[0];
+  md -= (int32_t)((PINV30 * (uint32_t)cd + (uint32_t)md) & (uint32_t)M30);
+  me -= (int32_t)((PINV30 * (uint32_t)ce + (uint32_t)me) & (uint32_t)M30);
+  cd += (int64_t)PL[0] * md;
+  ce += (int64_t)PL[0] * me;
+  cd >>= 30;
+  ce >>= 30;
+#pragma unroll
+  for (int i = 1; i < NL; ++i) {
+    cd += u * d[i] + v * e[i] + (int64_t)PL[i] * md;
+    ce += q * d[i] + r * e[i] + (int64_t)PL[i] * me;
+    d[i - 1] = (int32_t)cd & M30;
+    cd >>= 30;
+    e[i - 1] = (int32_t)ce & M30;
+    ce >>= 30;
+  }
+  d[NL - 1] = (int32_t)cd;
+  e[NL - 1] = (int32_t)ce;
+}
+
+// d in (-2p, p) -> (neg ? -d : d) in [0, p)
+OVH_HD void normalize(int32_t* d, bool neg) {
+  int32_t c = d[NL - 1] >> 31;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] += PL[i] & c;
+  const int32_t n = neg ? -1 : 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] = (d[i] ^ n) - n;
+#pragma unroll
+  for (int i = 0; i < NL - 1; ++i) {
+    d[i + 1] += d[i] >> 30;
+    d[i] &= M30;
+  }
+  c = d[NL - 1] >> 31;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) d[i] += PL[i] & c;
+#pragma unroll
+  for (int i = 0; i < NL - 1; ++i) {
+    d[i + 1] += d[i] >> 30;
+    d[i] &= M30;
+  }
+}
+}  // namespace inv
+
+OVH_HD void fp_inv_divsteps(Fp& r, const Fp& a, const Fp& r3) {
+  using namespace inv;
+  int32_t f[NL], g[NL], d[NL], e[NL];
+  uint32_t any = 0;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {  // 12 x 32 -> 13 x 30 bits
+    const int b = 30 * k, w = b >> 5, sh = b & 31;
+    uint32_t x = a.v[w] >> sh;
+    if (sh > 2 && w + 1 < 12) x |= a.v[w + 1] << (32 - sh);
+    g[k] = (int32_t)(x & (uint32_t)M30);
+    f[k] = PL[k];
+    d[k] = 0;
+    e[k] = 0;
+    any |= a.v[k < 12 ? k : 11];
+  }
+  e[0] = 1;
+  if (!any) {
+    fp_zero(r);
+    return;
+  }
+  int32_t eta = -1;
+#pragma unroll 1
+  for (int it = 0; it < 80; ++it) {  // converges in well under 1102 / 30 batches
+    Trans t;
+    eta = divsteps30(eta, (uint32_t)f[0], (uint32_t)g[0], t);
+    update_de(d, e, t);
+    update_fg(f, g, t);
+    if (g[0] == 0) {
+      int32_t z = 0;
+#pragma unroll
+      for (int i = 1; i < NL; ++i) z |= g[i];
+      if (z == 0) break;
+    }
+  }
+  normalize(d, f[NL - 1] < 0);
+  Fp x;
+#pragma unroll
+  for (int w = 0; w < 12; ++w) {  // 13 x 30 -> 12 x 32 bits
+    const int b = 32 * w, k = b / 30, sh = b % 30;
+    uint32_t y = (uint32_t)d[k] >> sh;
+    if (k + 1 < NL) y |= (uint32_t)d[k + 1] << (30 - sh);
+    if (sh > 28 && k + 2 < NL) y |= (uint32_t)d[k + 2] << (60 - sh);
+    x.v[w] = y;
+  }
+  fp_mul(r, x, r3);
+}
+
+// a^-1 (0 -> 0) by divsteps: ~37 batches of 30 steps on 13 x 30-bit limbs instead of the ~450
+// dependent products of a^(p-2) (k_g2p_compress and every other one-lane inversion)
+OVH_HD void fp_inv(Fp& r, const Fp& a) {
+  Fp c, r3;
+  uint32_t d[12], br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d[i] = subc32(a.v[i], P_LIMBS[i], br, &br);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) c.v[i] = br ? a.v[i] : d[i];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r3.v[i] = R3_M[i];
+  fp_inv_divsteps(r, c, r3);
+}
 
 // Square root candidate a^((p+1)/4); returns true iff it squares back to a.
 OVH_HD bool fp_sqrt(Fp& r, const Fp& a) {
