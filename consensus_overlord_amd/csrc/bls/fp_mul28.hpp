@@ -1,10 +1,14 @@
-// Montgomery product a b 2^-384 mod p on 14 x 28-bit limbs (see fp_mul28.hip). Interface of
+// Montgomery product a b 2^-384 mod p on 14 x 28-bit limbs, gfx950 device code. Interface of
 // fp_mul_gfx950: 12 x 32-bit limbs in / out, a, b < 4p, r < 1.63p after one conditional
-// subtraction.
+// subtraction. A column of 14 + 14 products of 28-bit limbs plus the carry stays below 2^61, so
+// every partial product is one v_mad_u64_u32 into a 64-bit accumulator, with no carry word
+// (the 12 x 32 product scanning pays one v_addc per v_mad). R = 2^392; a enters shifted left by
+// 8 bits, so the result is a b 2^-384 (the Montgomery form everywhere else is unchanged).
+// tools/ubench/fp_mul28.hip times it against fp_mul_gfx950 and checks them against each other.
 #pragma once
 #include <stdint.h>
 
-#include "../../consensus_overlord_amd/csrc/bls/consts.hpp"
+#include "consts.hpp"
 
 namespace ovh {
 
@@ -65,17 +69,13 @@ __device__ __forceinline__ void fp_mul28(uint32_t* r, const uint32_t* a, const u
   // u < 2.63 p: r = u - p unless that borrows
   uint32_t d[12], br = 0;
 #pragma unroll
-  for (int j = 0; j < 12; ++j) d[j] = subc32(u[j], P_LIMBS[j], br, &br);
+  for (int j = 0; j < 12; ++j) {
+    const uint64_t w = (uint64_t)u[j] - P_LIMBS[j] - br;
+    d[j] = (uint32_t)w;
+    br = (uint32_t)(w >> 63);
+  }
 #pragma unroll
   for (int j = 0; j < 12; ++j) r[j] = br ? u[j] : d[j];
-}
-
-__device__ __forceinline__ void vm_canon(Fp& r, const Fp& a) {
-  uint32_t d[12], br = 0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) d[j] = subc32(a.v[j], P_LIMBS[j], br, &br);
-#pragma unroll
-  for (int j = 0; j < 12; ++j) r.v[j] = br ? a.v[j] : d[j];
 }
 
 }  // namespace ovh

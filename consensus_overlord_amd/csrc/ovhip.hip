@@ -1942,8 +1942,8 @@ static int verify_host_locked(ovh_ctx* c, size_t n, const uint8_t* sigs, const u
   if (n == 1) {
     CHK(verify_one_locked(c, d, d + 96, staged_key(c, n, d, t, 0), dc));
   } else {
-    for (size_t lo : {(size_t)0, t}) {
-      const size_t cnt = lo == 0 ? t : n - t;
+    for (int part = 0; part < 2; ++part) {  // table votes [0, t), then the others [t, n)
+      const size_t lo = part ? t : 0, cnt = part ? n - t : t;
       if (!cnt) continue;
       CHK(verify_async_locked(c, cnt, d + 96 * lo, d + n * 96 + 32 * lo, staged_key(c, n, d, t, lo), dc + lo));
     }
@@ -2016,8 +2016,8 @@ static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
     CHK(stage_split(s, cnt, sigs + lo * 96, hashes + lo * 32, pks + lo * 48, &in, &t, perms[d]));
     dcodes[d] = (int32_t*)(in + cnt * 176);
     CHK(ensure_cap(s, cnt));
-    for (size_t plo : {(size_t)0, t}) {
-      const size_t pc = plo == 0 ? t : cnt - t;
+    for (int part = 0; part < 2; ++part) {  // table votes [0, t), then the others [t, cnt)
+      const size_t plo = part ? t : 0, pc = part ? cnt - t : t;
       if (!pc) continue;
       Part p{0, plo, pc};
       CHK(take_slot(s, &p.slot));
@@ -2180,8 +2180,8 @@ static int submit_host_single(ovh_ctx* c, size_t n, const uint8_t* sigs, const u
     CHK(verify_one_locked(c, in, in + 96, staged_key(c, n, in, t, 0), dc));
   } else {
     int prev = -1;
-    for (size_t lo : {(size_t)0, t}) {
-      const size_t cnt = lo == 0 ? t : n - t;
+    for (int part = 0; part < 2; ++part) {  // table votes [0, t), then the others [t, n)
+      const size_t lo = part ? t : 0, cnt = part ? n - t : t;
       if (!cnt) continue;
       CHK(verify_async_locked(c, cnt, in + 96 * lo, in + n * 96 + 32 * lo, staged_key(c, n, in, t, lo), dc + lo, true));
       if (prev >= 0) HIPCHK(hipStreamWaitEvent(c->fs[c->last_slot], c->ev_back[prev], 0));
@@ -2241,8 +2241,8 @@ static int submit_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
     CHK(ensure_cap(s, cnt));
     first.push_back(ps.size());
     int pi = 0;
-    for (size_t plo : {(size_t)0, t}) {
-      const size_t pc = plo == 0 ? t : cnt - t;
+    for (int part = 0; part < 2; ++part) {  // table votes [0, t), then the others [t, cnt)
+      const size_t plo = part ? t : 0, pc = part ? cnt - t : t;
       if (!pc) continue;
       int slot;
       CHK(take_slot(s, &slot));

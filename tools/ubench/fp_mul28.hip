@@ -11,7 +11,18 @@
 #include <stdio.h>
 
 #include "../../consensus_overlord_amd/csrc/bls/fp.hpp"
-#include "fp_mul28.hpp"
+#include "../../consensus_overlord_amd/csrc/bls/fp_mul28.hpp"
+
+namespace ovh {
+__device__ __forceinline__ void vm_canon(Fp& r, const Fp& a) {
+  uint32_t d[12], br = 0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) d[j] = subc32(a.v[j], P_LIMBS[j], br, &br);
+#pragma unroll
+  for (int j = 0; j < 12; ++j) r.v[j] = br ? a.v[j] : d[j];
+}
+
+}  // namespace ovh
 
 using namespace ovh;
 
