@@ -24,6 +24,7 @@
 #if defined(__HIP_DEVICE_COMPILE__)
 #include "fp_mul_gfx950.hpp"
 #include "fp_mul28.hpp"
+#include "fp_mul28_gfx950.hpp"
 #endif
 
 namespace ovh {
@@ -131,7 +132,9 @@ OVH_HD void fp_neg(Fp& r, const Fp& a) {
 
 // Montgomery product r = a * b * 2^-384 mod p (CIOS, no extra carry word: p[11] < 2^31).
 OVH_HD void fp_mul(Fp& r, const Fp& a, const Fp& b) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(OVH_FPMUL28)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(OVH_FPMUL28) && OVH_FPMUL28 == 2
+  fp_mul28_gfx950(r.v, a.v, b.v);
+#elif defined(__HIP_DEVICE_COMPILE__) && defined(OVH_FPMUL28)
   fp_mul28(r.v, a.v, b.v);
 #elif defined(__HIP_DEVICE_COMPILE__)
   fp_mul_gfx950(r.v, a.v, b.v);

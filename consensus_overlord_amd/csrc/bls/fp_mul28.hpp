@@ -35,6 +35,23 @@ __device__ __forceinline__ void split28(uint32_t* x, const uint32_t* a) {
   }
 }
 
+// 14 x 28 -> 12 x 32, then one conditional subtraction (the value is < 2.63 p)
+__device__ __forceinline__ void join28_reduce(uint32_t* r, const uint32_t* t) {
+  uint32_t u[12];
+#pragma unroll
+  for (int j = 0; j < 12; ++j) {
+    const int k = (32 * j) / 28, s = (32 * j) % 28;
+    uint32_t v = (t[k] >> s) | (t[k + 1] << (28 - s));
+    if (s > 24 && k + 2 < 14) v |= t[k + 2] << (56 - s);
+    u[j] = v;
+  }
+  uint32_t d[12], br = 0;
+#pragma unroll
+  for (int j = 0; j < 12; ++j) d[j] = __builtin_subc(u[j], P_LIMBS[j], br, &br);  // v_sub(b)_co chain
+#pragma unroll
+  for (int j = 0; j < 12; ++j) r[j] = br ? u[j] : d[j];
+}
+
 __device__ __forceinline__ void fp_mul28(uint32_t* r, const uint32_t* a, const uint32_t* b) {
   uint32_t x[14], y[14], m[14], t[14];
   split28<8>(x, a);  // a 2^8: with R = 2^392 the product is a b 2^-384
@@ -57,25 +74,7 @@ __device__ __forceinline__ void fp_mul28(uint32_t* r, const uint32_t* a, const u
     acc >>= 28;
   }
   t[13] = (uint32_t)acc;
-  // 14 x 28 -> 12 x 32
-  uint32_t u[12];
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    const int k = (32 * j) / 28, s = (32 * j) % 28;
-    uint32_t v = (t[k] >> s) | (t[k + 1] << (28 - s));
-    if (s > 24 && k + 2 < 14) v |= t[k + 2] << (56 - s);
-    u[j] = v;
-  }
-  // u < 2.63 p: r = u - p unless that borrows
-  uint32_t d[12], br = 0;
-#pragma unroll
-  for (int j = 0; j < 12; ++j) {
-    const uint64_t w = (uint64_t)u[j] - P_LIMBS[j] - br;
-    d[j] = (uint32_t)w;
-    br = (uint32_t)(w >> 63);
-  }
-#pragma unroll
-  for (int j = 0; j < 12; ++j) r[j] = br ? u[j] : d[j];
+  join28_reduce(r, t);
 }
 
 }  // namespace ovh

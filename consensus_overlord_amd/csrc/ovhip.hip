@@ -3227,10 +3227,10 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   }
   // pipelined: only hash_to_field + the vote kernel on the main stream; the fold levels, the MSM
   // and the packing on the slot's final stream (behind the residency gate), which the caller's
-  // stream then waits for (its all-gather, then ovh_combine_partials_device_async). The main
-  // stream first waits for the caller's stream: the inputs may still be in flight there.
-  HIPCHK(hipEventRecord(c->ev_x[0], st));
-  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_x[0], 0));
+  // stream then waits for (its all-gather, then ovh_combine_partials_device_async). The inputs
+  // are read in ovh_stream order (include/ovhip.h): waiting on `stream` here would also wait for
+  // the previous batch's gather and combine queued there and serialise the pipeline (r03b: 1,062k
+  // -> 796k verifs/s at one rank).
   CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false));
   hipStream_t fst = c->fs[slot];
   int reg;

@@ -44,6 +44,13 @@ class DeviceBackend:
     def empty_partials(self, world: int) -> torch.Tensor:
         return torch.empty((BATCH_SLOTS, world, PARTIAL_BYTES), dtype=torch.uint8, device="cuda")
 
+    def inputs_ready(self, producer) -> None:
+        """The library reads a batch's inputs in its own stream's order (ovh_stream,
+        include/ovhip.h): that stream waits for the producer stream's work so far -- not the
+        gather stream, which also carries the previous batch's combine."""
+        lib_stream = torch.cuda.ExternalStream(self.ctx.stream)
+        lib_stream.wait_stream(producer)
+
     def partial(self, sigs, hashes, pks, codes, out_row, index_base: int) -> None:
         self.dev.batch_partial(self.ctx, sigs, hashes, pks, codes, out_row, stream=self.stream)
 
@@ -83,7 +90,9 @@ class ShardVerifier:
         # tensors stay referenced until wait(), so the caching allocator cannot hand them out
         self._inflight.append((sigs, hashes, pks, codes))
         if st is not None:
-            st.wait_stream(torch.cuda.current_stream())   # the caller's inputs
+            cur = torch.cuda.current_stream()
+            self.backend.inputs_ready(cur)                 # the caller's inputs, for the library
+            st.wait_stream(cur)                            # and for the gather
             with torch.cuda.stream(st):
                 self._submit(part, sigs, hashes, pks, codes, index_base)
         else:

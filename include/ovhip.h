@@ -170,7 +170,9 @@ int ovh_verify_batch_device(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const
  * Stream order: `stream` (a hipStream_t of the caller, e.g. torch's current stream) -- the
  * partial is written after the work already on `stream` (so a gather buffer can be reused) and
  * `stream` waits for the write; the call returns without blocking. stream NULL: the call
- * returns once d_partial is written. */
+ * returns once d_partial is written. The inputs (d_sigs, d_hashes, d_pks) are read in
+ * ovh_stream(ctx) order: a caller that produced them on another stream first makes ovh_stream
+ * wait for it (shard.py does, through an event). */
 #define OVH_PARTIAL_BYTES 864
 int ovh_batch_partial_device(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
                              const uint8_t* d_pks, int32_t* d_codes, uint8_t* d_partial, void* stream);

@@ -12,6 +12,7 @@
 
 #include "../../consensus_overlord_amd/csrc/bls/fp.hpp"
 #include "../../consensus_overlord_amd/csrc/bls/fp_mul28.hpp"
+#include "../../consensus_overlord_amd/csrc/bls/fp_mul28_gfx950.hpp"
 
 namespace ovh {
 __device__ __forceinline__ void vm_canon(Fp& r, const Fp& a) {
@@ -35,7 +36,8 @@ __global__ __launch_bounds__(64) void k_chain(uint32_t iters, uint32_t* out) {
   }
   for (uint32_t i = 0; i < iters; ++i) {
     if (V == 0) fp_mul(x, x, y);
-    else fp_mul28(x.v, x.v, y.v);
+    else if (V == 1) fp_mul28(x.v, x.v, y.v);
+    else fp_mul28_gfx950(x.v, x.v, y.v);
   }
   Fp c;
   vm_canon(c, x);
@@ -52,24 +54,25 @@ int main() {
   const uint32_t iters = 2048;
   static uint32_t h0[4096 * 64 * 12], h1[4096 * 64 * 12];
   for (int grid : {1024, 4096}) {
-    float t[2];
-    for (int v = 0; v < 2; ++v) {
-      auto k = v == 0 ? k_chain<0> : k_chain<1>;
-      hipLaunchKernelGGL(k, dim3(grid), dim3(64), 0, 0, iters, v == 0 ? d0 : d1);
+    float t[3];
+    size_t bad[3] = {0, 0, 0};
+    for (int v = 0; v < 3; ++v) {
+      auto k = v == 0 ? k_chain<0> : v == 1 ? k_chain<1> : k_chain<2>;
+      uint32_t* d = v == 0 ? d0 : d1;
+      hipLaunchKernelGGL(k, dim3(grid), dim3(64), 0, 0, iters, d);
       (void)hipDeviceSynchronize();
       (void)hipEventRecord(a);
-      hipLaunchKernelGGL(k, dim3(grid), dim3(64), 0, 0, iters, v == 0 ? d0 : d1);
+      hipLaunchKernelGGL(k, dim3(grid), dim3(64), 0, 0, iters, d);
       (void)hipEventRecord(b);
       (void)hipEventSynchronize(b);
       (void)hipEventElapsedTime(&t[v], a, b);
+      (void)hipMemcpy(v == 0 ? h0 : h1, d, grid * 64 * 48, hipMemcpyDeviceToHost);
+      if (v)
+        for (size_t i = 0; i < (size_t)grid * 64 * 12; ++i) bad[v] += h0[i] != h1[i];
     }
-    (void)hipMemcpy(h0, d0, grid * 64 * 48, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(h1, d1, grid * 64 * 48, hipMemcpyDeviceToHost);
-    size_t bad = 0;
-    for (size_t i = 0; i < (size_t)grid * 64 * 12; ++i) bad += h0[i] != h1[i];
-    printf("{\"waves\": %d, \"ns_per_mul_32x12\": %.1f, \"ns_per_mul_28x14\": %.1f, \"speedup\": %.3f, "
-           "\"mismatched_words\": %zu}\n",
-           grid, t[0] * 1e6 / iters, t[1] * 1e6 / iters, t[0] / t[1], bad);
+    printf("{\"waves\": %d, \"ns_per_mul_32x12\": %.1f, \"ns_per_mul_28x14_cpp\": %.1f, \"ns_per_mul_28x14_asm\": "
+           "%.1f, \"speedup_cpp\": %.3f, \"speedup_asm\": %.3f, \"mismatched_words\": [%zu, %zu]}\n",
+           grid, t[0] * 1e6 / iters, t[1] * 1e6 / iters, t[2] * 1e6 / iters, t[0] / t[1], t[0] / t[2], bad[1], bad[2]);
   }
   return 0;
 }
