@@ -130,14 +130,15 @@ OVH_HD void fp_neg(Fp& r, const Fp& a) {
   fp_sub(r, z, a);
 }
 
-// Montgomery product r = a * b * 2^-384 mod p (CIOS, no extra carry word: p[11] < 2^31).
+// Montgomery product r = a * b * 2^-384 mod p. Device: fp_mul28_gfx950 (14 x 28-bit limbs, one
+// 64-bit accumulator per column, no carry word). Host: CIOS on 12 x 32-bit limbs (p[11] < 2^31).
 OVH_HD void fp_mul(Fp& r, const Fp& a, const Fp& b) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(OVH_FPMUL28) && OVH_FPMUL28 == 2
-  fp_mul28_gfx950(r.v, a.v, b.v);
-#elif defined(__HIP_DEVICE_COMPILE__) && defined(OVH_FPMUL28)
-  fp_mul28(r.v, a.v, b.v);
+#if defined(__HIP_DEVICE_COMPILE__) && defined(OVH_FPMUL32)
+  fp_mul_gfx950(r.v, a.v, b.v);  // A/B builds: the 12 x 32-bit product scanning form
 #elif defined(__HIP_DEVICE_COMPILE__)
-  fp_mul_gfx950(r.v, a.v, b.v);
+  // 14 x 28-bit limbs, one 64-bit accumulator (r03c: vote kernel 3.76 -> 3.56 ms, 1,060k ->
+  // 1,115k verifs/s; tools/ubench/fp_mul28.hip 1.10-1.14x per product)
+  fp_mul28_gfx950(r.v, a.v, b.v);
 #else
   OVH_COUNT_MUL();
   uint32_t t[12];

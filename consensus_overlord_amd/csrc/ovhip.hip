@@ -2265,16 +2265,18 @@ static int submit_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
   }
   // the combined check on the batch's final device
   HIPCHK(hipSetDevice(F->device));
-  for (const Part& p : ps) HIPCHK(hipStreamWaitEvent(F->fstream, p.s->ev_m[j][p.pi], 0));
+  // consecutive batches' combined checks alternate between the final device's two final streams
+  const hipStream_t fin = (root->hb_k & 1) ? F->fstream2 : F->fstream;
+  for (const Part& p : ps) HIPCHK(hipStreamWaitEvent(fin, p.s->ev_m[j][p.pi], 0));
   Slab PF, PS;
   uint32_t m;
-  CHK(stage_partials(F, F->fstream, k, gather, F->fin + (size_t)j * FIN_STRIDE, &PF, &PS, &m));
+  CHK(stage_partials(F, fin, k, gather, F->fin + (size_t)j * FIN_STRIDE, &PF, &PS, &m));
   int32_t* fv = F->result + RES_MULTI + 1 + j;
-  enqueue_final(F, F->fstream, PF, PS, m, fv);
+  enqueue_final(F, fin, PF, PS, m, fv);
   for (size_t q : first)
     if (ps[q].s != F)
-      HIPCHK(hipMemcpyPeerAsync(ps[q].s->result + RES_MULTI + 1 + j, ps[q].s->device, fv, F->device, 4, F->fstream));
-  HIPCHK(hipEventRecord(F->ev_m[j][2], F->fstream));
+      HIPCHK(hipMemcpyPeerAsync(ps[q].s->result + RES_MULTI + 1 + j, ps[q].s->device, fv, F->device, 4, fin));
+  HIPCHK(hipEventRecord(F->ev_m[j][2], fin));
   // per device: device-gated bisection of its parts, then the codes into the pinned buffer
   for (size_t e = 0; e < first.size(); ++e) {
     const Part& p0 = ps[first[e]];

@@ -156,11 +156,30 @@ JAC_COFACTOR = True
 YAO_POW = True        # sqrt_ratio's exponentiation by Yao's method (f2_pow_frob_yao)   # cofactor clearing's [|x|] chains in Jacobian coordinates (see g2_jac_dbl)
 
 
+# RFC 9380 I.3 sqrt for q = 9 (mod 16), q = p^2: c1 = sqrt(-1) = u, c2 = sqrt(c1), c3 = sqrt(-c1)
+SQ9_C2 = (0x6af0e0437ff400b6831e36d6bd17ffe48395dabc2d3435e77f76e17009241c5ee67992f72ec05f4c81084fbede3cc09,
+          0x135203e60180a68ee2e9c448d77a2cd91c3dedd930b1cf60ef396489f61eb45e304466cf3e67fa0af1ee7b04121bdea2)
+SQ9_C3 = (0x6af0e0437ff400b6831e36d6bd17ffe48395dabc2d3435e77f76e17009241c5ee67992f72ec05f4c81084fbede3cc09,
+          0x6af0e0437ff400b6831e36d6bd17ffe48395dabc2d3435e77f76e17009241c5ee67992f72ec05f4c81084fbede3cc09)
+SQ9_C4 = (P * P + 7) // 16
+
+
+def _f2m(a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+
+assert _f2m(SQ9_C2, SQ9_C2) == (0, 1) and _f2m(SQ9_C3, SQ9_C3) == (0, P - 1)
+
+
 class Alg:
-    def __init__(self, prog: Prog, inv_op: bool = False, use_sop: bool = False):
+    def __init__(self, prog: Prog, inv_op: bool = False, use_sop: bool = False, fast_sqrt: bool = False):
         self.p = prog
         self.use_sop = use_sop   # Fp2 products as two sum-of-products ops (ir.Prog.sop)
         self.inv_op = inv_op   # Fp inversion by the interpreter's one-lane binary Euclid
+        # Fp2 square roots by one Frobenius-split Yao exponentiation (f2_sqrt9): ~390 dependent
+        # levels instead of the norm method's two Fp chains (~760), ~300 more products -- the
+        # latency programs (one signature or one vote on the GPU) take it
+        self.fast_sqrt = fast_sqrt
 
     # ---------------------------------------------------------------- Fp
     def c(self, v):
@@ -196,6 +215,43 @@ class Alg:
             acc = odd[val >> 1] if acc is None else acc * odd[val >> 1]
             i = j
         return acc
+
+    def fp_pow_yao(self, a, e: int, w: int = 3, LAG: int = 2):
+        """a^e by Yao's right-to-left k-ary method (as f2_pow_frob_yao, in Fp): the squaring
+        chain B_j = a^(2^(w j)) carries the critical path, each window digit d multiplies B_j
+        into an accumulator X_d off that path, prod_d X_d^d closes."""
+        pp = self.p
+        mask = (1 << w) - 1
+        nwin = (e.bit_length() + w - 1) // w
+        X = [None] * (1 << w)
+        B = a
+        done = []
+        for j in range(nwin):
+            if j:
+                deps = done[j - 1 - LAG] if j - 1 - LAG >= 0 else []
+                if deps:   # the chain at most LAG windows ahead of the accumulations
+                    B = pp._op("muls", (B.id, None, B.id, None), (1, 0, 1, 0), deps=tuple(v.id for v in deps))
+                else:
+                    B = B * B
+                for _ in range(w - 1):
+                    B = B * B
+            d = (e >> (w * j)) & mask
+            got = []
+            if d:
+                X[d] = B if X[d] is None else X[d] * B
+                got.append(X[d])
+            done.append(got)
+        ys, y = [], None
+        for d in range(mask, 0, -1):
+            if X[d] is None:
+                if y is not None:
+                    ys.append(y)
+                continue
+            y = X[d] if y is None else y * X[d]
+            ys.append(y)
+        while len(ys) > 1:
+            ys = [ys[k] * ys[k + 1] if k + 1 < len(ys) else ys[k] for k in range(0, len(ys), 2)]
+        return ys[0]
 
     def fp_inv(self, a):
         if self.inv_op:
@@ -432,6 +488,23 @@ class Alg:
         r = (x0, x1)
         ok = self.f2_eq(self.f2_sqr(r), a)
         return ok, r
+
+    def f2_sqrt9(self, a):
+        """RFC 9380 Appendix I.3 (q = p^2 = 9 mod 16): z = a^((q+7)/16) times the 8th root of
+        unity that makes z^2 = a when a is a square (f2_pow_frob_yao carries the exponentiation).
+        Returns (ok, root); ok iff a is a square."""
+        p = self.p
+        tv1 = self.f2_pow_frob_yao(a, SQ9_C4)
+        tv2 = (-tv1[1], tv1[0])                 # c1 tv1 = u tv1
+        tv3 = self.f2_mul(tv1, self.c2(SQ9_C2))
+        tv4 = self.f2_mul(tv1, self.c2(SQ9_C3))
+        e1 = self.f2_eq(self.f2_sqr(tv2), a)
+        e2 = self.f2_eq(self.f2_sqr(tv3), a)
+        tv1 = self.f2_sel(e1, tv1, tv2)
+        tv2 = self.f2_sel(e2, tv4, tv3)
+        e3 = self.f2_eq(self.f2_sqr(tv2), a)
+        z = self.f2_sel(e3, tv1, tv2)
+        return self.f2_eq(self.f2_sqr(z), a), z
 
     # ---------------------------------------------------------------- Fp6 / Fp12
     def f6_add(self, a, b):
@@ -748,7 +821,7 @@ class Alg:
         p = self.p
         x = x_plain
         rhs = p.lin4(x * (x * x), 1, p.const(4), 1, None)
-        y = self.fp_pow(rhs, (P + 1) // 4)
+        y = self.fp_pow_yao(rhs, (P + 1) // 4) if self.fast_sqrt else self.fp_pow(rhs, (P + 1) // 4)
         ok = p.eq(y * y, rhs)
         flip = p.f_xor(p.lex(y), sort_flag)
         y = p.sel(flip, y, -y)
@@ -757,7 +830,7 @@ class Alg:
     def g2_decompress(self, x, sort_flag):
         p = self.p
         rhs = self.f2_add(self.f2_mul(x, self.f2_sqr(x)), self.c2((4, 4)))
-        ok, y = self.f2_sqrt(rhs)
+        ok, y = self.f2_sqrt9(rhs) if self.fast_sqrt else self.f2_sqrt(rhs)
         flip = p.f_xor(self.f2_lex(y), sort_flag)
         y = self.f2_sel(flip, y, self.f2_neg(y))
         return ok, (x, y)

@@ -31,6 +31,8 @@ layouts. Input and output names are listed in the order the HIP side addresses t
 """
 from __future__ import annotations
 
+import os
+
 
 from alg import G1X, G1Y, Alg
 from ir import P, Prog
@@ -67,6 +69,9 @@ def unflat_g2p(v):
 # HBM state planes of a vote (ovhip.hip reads them through VM_S_* in vm_progs.inc):
 # u0, u1 | sigma affine | tau = -psi^2(sigma) affine | f | r sigma (bisection only)
 S_U, S_SIG, S_TAU, S_F, S_RS, S_TOTAL = 0, 4, 8, 12, 24, 30
+# square roots by one Yao exponentiation (alg.Alg fast_sqrt) in the batch vote programs too:
+# vote 2,985 -> 2,824 phases, vote_t 2,972 -> 2,629 (cost estimate -4% / -11%)
+FAST_SQRT_BATCH = os.environ.get("OVH_FAST_SQRT_BATCH", "1") == "1"
 
 VOTE_IN = ["pk_x", "pk_sort", "sig_x0", "sig_x1", "sig_sort", "u00", "u01", "u10", "u11"]
 VOTE_OUT = ["pk_ok", "pk_grp", "sig_ok", "sig_grp", "h_inf"]
@@ -83,7 +88,7 @@ def affine_pair(a, Q):
 
 def build_vote():
     p = Prog("vote")
-    a = Alg(p, use_sop=USE_SOP)
+    a = Alg(p, use_sop=USE_SOP, fast_sqrt=FAST_SQRT_BATCH)
     R = p.const(R_MONT)
     pkx = p.input("pk_x") * R
     sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
@@ -114,7 +119,7 @@ VOTE_T_OUT = ["sig_ok", "sig_grp", "h_inf"]
 
 def build_vote_t():
     p = Prog("vote_t")
-    a = Alg(p, use_sop=USE_SOP)
+    a = Alg(p, use_sop=USE_SOP, fast_sqrt=FAST_SQRT_BATCH)
     R = p.const(R_MONT)
     Pp = (p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z"))
     sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
@@ -142,7 +147,7 @@ VOTE1_ST = [(n, S_F + k) for k, n in enumerate(f12_names("f"))]
 def build_vote1(table: bool):
     def build():
         p = Prog("vote_t1" if table else "vote1")
-        a = Alg(p, use_sop=USE_SOP)
+        a = Alg(p, use_sop=USE_SOP, fast_sqrt=True)
         R = p.const(R_MONT)
         if table:
             Pa = (p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z"))
@@ -258,7 +263,7 @@ SIGCHK_OUT = ["sig_ok", "sig_grp", "q0", "q1", "q2", "q3"]
 
 def build_sigchk():
     p = Prog("sigchk")
-    a = Alg(p, use_sop=USE_SOP)
+    a = Alg(p, use_sop=USE_SOP, fast_sqrt=True)
     R = p.const(R_MONT)
     sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
     sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
@@ -274,7 +279,7 @@ PKCHK_OUT = ["pk_ok", "pk_grp", "p0", "p1"]
 
 def build_pkchk():
     p = Prog("pkchk")
-    a = Alg(p, use_sop=USE_SOP)
+    a = Alg(p, use_sop=USE_SOP, fast_sqrt=True)
     R = p.const(R_MONT)
     pk_ok, (px, py) = a.g1_decompress(p.input("pk_x") * R, p.input("pk_sort"))
     pk_grp, _ = a.g1_in_group((px, py, p.one))

@@ -12,8 +12,8 @@ timeout -k 10 300 python -c "import torch; print(torch.__version__, torch.cuda.i
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 timeout -k 10 300 python -u bench.py --steps ${STEPS:-30} --warmup 2 > "$OUT/bench.log" 2>&1
-if [ -n "${M28:-}" ]; then
-  OVH_LIBPATH=$R/consensus_overlord_amd/libovhip_m28.so timeout -k 10 200 python -u bench.py --steps ${STEPS:-30} --warmup 2 --no-cpu-baseline > "$OUT/bench_m28.log" 2>&1
+if [ -n "${AB:-}" ]; then
+  OVH_LIBPATH=$R/consensus_overlord_amd/libovhip_ab.so timeout -k 10 200 python -u bench.py --steps ${STEPS:-30} --warmup 2 --no-cpu-baseline > "$OUT/bench_ab.log" 2>&1
 fi
 if [ -n "${Q8:-}" ]; then
   GPU_MAX_HW_QUEUES=8 timeout -k 10 200 python -u bench.py --steps ${STEPS:-30} --warmup 2 --no-cpu-baseline --no-latency > "$OUT/bench_q8.log" 2>&1
