@@ -41,7 +41,11 @@
 #include "keygen.hpp"
 #include "rlp.hpp"
 #include "sm3.hpp"
+#ifdef OVH_VM_PROGS
+#include OVH_VM_PROGS  // A/B builds: another generation of the programs
+#else
 #include "vm_progs.inc"
+#endif
 static_assert(VM_KZERO == ovh::vm::KZERO && VM_KTAB == ovh::vm::KTAB, "fixed constants (tools/fpvm/gen.py)");
 
 using namespace ovh;
@@ -220,9 +224,14 @@ struct VmDev {  // a program in device memory
 // 128-byte boundary and repeat at 128-byte strides, so slot s and constant c share LDS banks
 // exactly when s = c (mod 8) -- the rule tools/fpvm/sched.py spreads operand reads by.
 constexpr uint32_t align128w(uint32_t w) { return (w + 31) / 32 * 32; }
-constexpr uint32_t SLOT_BASE_W = align128w(VM_NCONST * 12);
-constexpr uint32_t VOTE_STRIDE_W = align128w(VM_VOTE_NSLOTS * 12 + 4);  // + 4 header words
-constexpr uint32_t VOTE_T_STRIDE_W = align128w(VM_VOTE_T_NSLOTS * 12 + 4);
+// 256-byte alignment (one LDS row of 64 banks): slot s of every slice and constant c then sit in
+// bank groups (3 s) and (3 c) mod 16 -- the model tools/fpvm/sched.py allocates slots by. A
+// ds_read_b128 lane group of a 16-lane program spans two slices ({0-3,12-15} of one and {4-11}
+// of the next), which only share that model when the slice stride is a multiple of 256 B.
+constexpr uint32_t align256w(uint32_t w) { return (w + 63) / 64 * 64; }
+constexpr uint32_t SLOT_BASE_W = align256w(VM_NCONST * 12);
+constexpr uint32_t VOTE_STRIDE_W = align256w(VM_VOTE_NSLOTS * 12 + 4);  // + 4 header words
+constexpr uint32_t VOTE_T_STRIDE_W = align256w(VM_VOTE_T_NSLOTS * 12 + 4);
 constexpr uint32_t FOLD_STRIDE_W = align128w(VM_FOLD_NSLOTS * 12);
 #define VM_FOLD_UNITS (64 / VM_FOLD_W)  // fold units per 64-lane workgroup
 
@@ -680,7 +689,7 @@ __global__ __launch_bounds__(64) void k_vm_votechk(uint32_t n, VmDev prog, const
 // Bisection, first step (skipped when *verdict == 1): r_i sigma_i of every vote with code 0 from
 // its stored sigma / tau (program "rs", the vote's RLC value) -> S_RS planes, for the group and
 // per-vote checks (the batch path sums these terms by the MSM instead).
-constexpr uint32_t RS_STRIDE_W = align128w(VM_RS_NSLOTS * 12);
+constexpr uint32_t RS_STRIDE_W = align256w(VM_RS_NSLOTS * 12);
 __global__ __launch_bounds__(64) void k_vm_rs(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g, Slab s,
                                               uint64_t seed, uint64_t base, const int32_t* __restrict__ codes,
                                               const int32_t* __restrict__ verdict) {
@@ -707,7 +716,7 @@ __global__ __launch_bounds__(64) void k_vm_rs(uint32_t n, VmDev prog, const uint
 // aggregate_signatures (consensus.rs:418-444) on the VM: one 96-byte signature per 16-lane slice
 // (program "sigchk": decompression + G2 subgroup check) -> the code k_parse_sig_list gives and
 // sigma projective (Z = 1; the identity for infinity or a failure) in planes 0..5 of `pts`.
-constexpr uint32_t SIGCHK_STRIDE_W = align128w(VM_SIGCHK_NSLOTS * 12 + 4);
+constexpr uint32_t SIGCHK_STRIDE_W = align256w(VM_SIGCHK_NSLOTS * 12 + 4);
 __global__ __launch_bounds__(64) void k_vm_sigchk(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
                                                   const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
                                                   int gc, int32_t* __restrict__ codes, Slab pts) {
@@ -815,7 +824,7 @@ __global__ __launch_bounds__(64) void k_g2p_compress(Slab in, uint8_t* out) {
 // selb bits of each launch, so the instruction stream does not depend on it. Lane 0 of the
 // slice compresses the result.
 constexpr uint32_t SIGN_NSLOTS = VM_SIGN0_NSLOTS > VM_SIGN1_NSLOTS ? VM_SIGN0_NSLOTS : VM_SIGN1_NSLOTS;
-constexpr uint32_t SIGN_STRIDE_W = align128w(SIGN_NSLOTS * 12 + 24 * 12);  // + acc, H, 2H, 3H stash
+constexpr uint32_t SIGN_STRIDE_W = align256w(SIGN_NSLOTS * 12 + 24 * 12);  // + acc, H, 2H, 3H stash
 __global__ __launch_bounds__(64) void k_vm_sign(uint32_t n, VmDev p0, VmDev p1, const uint32_t* __restrict__ cst_g,
                                                 const uint8_t* __restrict__ sks, Slab s, uint8_t* __restrict__ out) {
   static_assert(VM_SIGN0_W == VM_SIGN1_W && VM_SIGN0_NOUT == 24 && VM_SIGN1_NIN == 24 && VM_SIGN1_NOUT == 6,
@@ -903,7 +912,7 @@ __global__ __launch_bounds__(64) void k_gate(const unsigned long long* vstart, u
 // compressed key per 16-lane slice (program "pkchk": decompression + G1 subgroup check) -> flags
 // + the point (X : Y : Z) Montgomery, (0 : 1 : 0) for infinity or a failed parse. Flag precedence
 // as the vote kernel's (k_vm_vote): bad encoding, off the curve or x = 0 -> PKF_PARSE.
-constexpr uint32_t PKCHK_STRIDE_W = align128w(VM_PKCHK_NSLOTS * 12 + 4);
+constexpr uint32_t PKCHK_STRIDE_W = align256w(VM_PKCHK_NSLOTS * 12 + 4);
 __global__ __launch_bounds__(64) void k_vm_pkchk(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
                                                  const uint8_t* __restrict__ pks, Slab pts, uint32_t* __restrict__ flags) {
   extern __shared__ uint4 lds4[];

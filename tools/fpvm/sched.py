@@ -31,6 +31,8 @@ CONST_BASE = 0x800
 ABSENT = 0xFFFF
 # LDS pass width (lanes) and slot residues that share banks (OVH_BANK="lanes,mod" for A/B builds)
 BANK_LANES, BANK_MOD = (int(x) for x in os.environ.get("OVH_BANK", "16,16").split(","))
+# passes of the bank-conflict local search over the slot assignment (improve_banks; 0 = off)
+BANK_PASSES = int(os.environ.get("OVH_BANK_PASSES", "3"))
 # every lin op in the general-coefficient form (fpvm.hpp lin_mad): one linear block per phase
 # instead of the unit-sign block plus the general one; measured faster even for unit sums with
 # negations (r02aj: 1,013k -> 1,031-1,038k verifs/s). OVH_GEN_UNITLIN=1 with an interpreter
@@ -281,12 +283,101 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
                 alloc(i)
     if max_slots is not None and nslots > max_slots:
         raise RuntimeError("%s: %d slots > %d" % (prog.name, nslots, max_slots))
+    if BANK_PASSES and W == BANK_LANES:
+        improve_banks(prog, rounds, slot_of, def_round, last_use, nslots, consts, BANK_PASSES)
     for i in pre:
         if ops[i].kind == "const":
             consts.ref(ops[i].imm, ops[i].name == "raw")
     sc = Scheduled(prog, W, rounds, slot_of, nslots, consts)
     sc.kinds = kinds
     return sc
+
+
+def improve_banks(prog, rounds, slot_of, def_round, last_use, nslots, consts, passes):
+    """Local search over the slot assignment against the ds_read_b128 bank model (the whole
+    W-lane phase is one lane group; slot s and constant c hit bank group s, c mod BANK_MOD):
+    a read costs max over residues of the distinct addresses with that residue, minus one, in
+    extra LDS cycles. A value moves to a slot that is free over its whole lifetime [def, last
+    use] when that lowers the summed cost of the reads it takes part in. The slot count does not
+    change."""
+    import bisect
+    ops = prog.ops
+    zero_c = consts.ref(0, False) - CONST_BASE
+    ctx = defaultdict(list)        # (t, pos) -> operand keys ('v', id) / ('c', index)
+    reads_of = defaultdict(set)    # value -> contexts it is read in
+    for t, r in enumerate(rounds):
+        for i in r:
+            A, B, C, D = lane_operands(prog, i)[:4]
+            refs = [(1, B), (2, C)] if ops[i].kind == "selb" else list(enumerate((A, B, C, D)))
+            for pos, v in refs:
+                if v is not None and ops[v].kind != "const":
+                    key = ("v", v)
+                    reads_of[v].add((t, pos))
+                else:
+                    c = zero_c if v is None else consts.ref(ops[v].imm, ops[v].name == "raw") - CONST_BASE
+                    key = ("c", c)
+                if key not in ctx[(t, pos)]:
+                    ctx[(t, pos)].append(key)
+
+    def res(key, moved=None, r=None):
+        if key[0] == "c":
+            return key[1] % BANK_MOD
+        if key[1] == moved:
+            return r
+        return slot_of[key[1]] % BANK_MOD
+
+    def cost(c, moved=None, r=None):
+        cnt = [0] * BANK_MOD
+        for key in ctx[c]:
+            cnt[res(key, moved, r)] += 1
+        return max(cnt) - 1
+    # occupancy: per slot the sorted lifetimes of its values
+    occ = defaultdict(list)
+    for v, sl in slot_of.items():
+        occ[sl].append((def_round.get(v, -1), max(last_use[v], def_round.get(v, -1)), v))
+    for sl in occ:
+        occ[sl].sort()
+
+    def free_over(sl, lo, hi, v):
+        lst = occ[sl]
+        k = bisect.bisect_left(lst, (lo, -10 ** 9, -1))
+        for j in (k - 1, k):
+            if 0 <= j < len(lst):
+                a, b, u = lst[j]
+                if u != v and not (b < lo or a > hi):
+                    return False
+        return True
+    total = sum(cost(c) for c in ctx)
+    for _ in range(passes):
+        moved_any = 0
+        order = sorted(reads_of, key=lambda v: -sum(cost(c) for c in reads_of[v]))
+        for v in order:
+            cur = slot_of[v]
+            base = sum(cost(c) for c in reads_of[v])
+            if base == 0:
+                continue
+            lo, hi = def_round.get(v, -1), max(last_use[v], def_round.get(v, -1))
+            best = None
+            for r in sorted(range(BANK_MOD), key=lambda r: sum(cost(c, v, r) for c in reads_of[v])):
+                gain = base - sum(cost(c, v, r) for c in reads_of[v])
+                if gain <= 0:
+                    break
+                for sl in range(r, nslots, BANK_MOD):
+                    if sl != cur and free_over(sl, lo, hi, v):
+                        best = (sl, gain)
+                        break
+                if best:
+                    break
+            if best:
+                sl, gain = best
+                occ[cur] = [x for x in occ[cur] if x[2] != v]
+                bisect.insort(occ[sl], (lo, hi, v))
+                slot_of[v] = sl
+                total -= gain
+                moved_any += 1
+        if not moved_any:
+            break
+    return total
 
 
 def _operand(sc, v):
@@ -384,9 +475,12 @@ def encode(sc):
     LW = sc.prog.lin_width
     for r in sc.rounds:
         lanes = list(r) + [None] * (sc.W - len(r))
+        first = len(words)
         for i in lanes:
             if i is None:
-                words += [0] * nw
+                # an idle lane loads the operands of lane 0 (same addresses: an LDS broadcast,
+                # no extra bank conflict) and runs no op (opcode NOP, header bits of its own: none)
+                words += [0, words[first + 1], words[first + 2], 0] if nw == 4 and len(words) > first else [0] * nw
                 continue
             op = ops[i]
             k = op.kind
