@@ -69,8 +69,47 @@ VM_FN const uint4* slot_ptr(const uint32_t* __restrict__ slots, const uint32_t* 
 
 // the four operands of a phase, loaded limb-quarter-major (B, D, A, C for limbs 0..3, then 4..7,
 // then 8..11): the pre-add / lin chains start on the low limbs while the rest is in flight
+#if defined(__HIPCC__)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(3))) uint32_t* lds_cptr;
+VM_FN uint32_t lds_addr(const uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst, uint32_t ref) {
+  return (uint32_t)(uintptr_t)(lds_cptr)(((ref & CONST_BASE) ? cst : slots) + (ref & (CONST_BASE - 1)) * 12);
+}
+VM_FN void unpack4(Fp& r, int q, const u32x4 v) {
+  r.v[4 * q] = v.x; r.v[4 * q + 1] = v.y; r.v[4 * q + 2] = v.z; r.v[4 * q + 3] = v.w;
+}
+#endif
+
 VM_FN void ld_slots4(Fp& A, Fp& B, Fp& C, Fp& D, const uint32_t* __restrict__ slots,
                      const uint32_t* __restrict__ cst, uint32_t ra, uint32_t rb, uint32_t rc, uint32_t rd) {
+#if defined(__HIPCC__) && !defined(OVH_VM_CC_LOADS)
+  // The twelve reads are issued in one asm statement and waited for in three (one per limb
+  // quarter), so the compiler's waitcnt pass sees no LDS loads here: left to it, the loop's back
+  // edge merged these loads' pending state with the stores the phase ends with and it put an
+  // lgkmcnt(0) before the next phase's reads -- a full LDS round trip for the stores, every phase.
+  // LDS operations of a wave complete in order, so lgkmcnt(8 / 4 / 0) right after the reads
+  // guarantee the first 4 / 8 / 12 of them (and everything older) are done.
+  const uint32_t xa = lds_addr(slots, cst, ra), xb = lds_addr(slots, cst, rb), xc = lds_addr(slots, cst, rc),
+                 xd = lds_addr(slots, cst, rd);
+  u32x4 b0, d0, a0, c0, b1, d1, a1, c1, b2, d2, a2, c2;
+  asm volatile(
+      "ds_read_b128 %0, %12\n\tds_read_b128 %1, %13\n\tds_read_b128 %2, %14\n\tds_read_b128 %3, %15\n\t"
+      "ds_read_b128 %4, %12 offset:16\n\tds_read_b128 %5, %13 offset:16\n\t"
+      "ds_read_b128 %6, %14 offset:16\n\tds_read_b128 %7, %15 offset:16\n\t"
+      "ds_read_b128 %8, %12 offset:32\n\tds_read_b128 %9, %13 offset:32\n\t"
+      "ds_read_b128 %10, %14 offset:32\n\tds_read_b128 %11, %15 offset:32"
+      : "=&v"(b0), "=&v"(d0), "=&v"(a0), "=&v"(c0), "=&v"(b1), "=&v"(d1), "=&v"(a1), "=&v"(c1), "=&v"(b2),
+        "=&v"(d2), "=&v"(a2), "=&v"(c2)
+      : "v"(xb), "v"(xd), "v"(xa), "v"(xc)
+      : "memory");
+  asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(b0), "+v"(d0), "+v"(a0), "+v"(c0));
+  unpack4(B, 0, b0); unpack4(D, 0, d0); unpack4(A, 0, a0); unpack4(C, 0, c0);
+  asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(b1), "+v"(d1), "+v"(a1), "+v"(c1));
+  unpack4(B, 1, b1); unpack4(D, 1, d1); unpack4(A, 1, a1); unpack4(C, 1, c1);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b2), "+v"(d2), "+v"(a2), "+v"(c2));
+  unpack4(B, 2, b2); unpack4(D, 2, d2); unpack4(A, 2, a2); unpack4(C, 2, c2);
+  return;
+#endif
   const uint4 *pa = slot_ptr(slots, cst, ra), *pb = slot_ptr(slots, cst, rb), *pc = slot_ptr(slots, cst, rc),
               *pd = slot_ptr(slots, cst, rd);
 #pragma unroll
@@ -306,11 +345,10 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
   Fp A, B, C, D;
   ld_slots4(A, B, C, D, slots, cst, ra, rb, rc, in.z >> 16);
   const bool is_mul = op == OP_MULS || op == OP_SGN0 || op == OP_LEX || op == OP_EQ;
-#ifndef OVH_VM_UNIT_LIN
-  const bool lin_unit = false;  // every lin op runs lin_mad (tools/fpvm/sched.py ALL_ACC)
-#else
-  const bool lin_unit = ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 && cd <= 1;
-#endif
+  // unit sums run the add-chain block unless the encoder forced the general block (a linear
+  // phase runs one block: tools/fpvm/sched.py PHASE_UNIT, FORCE_ACC = w3 bit 24)
+  const bool lin_unit = !(in.w & (1u << 24)) && ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 &&
+                        cd <= 1;
   const bool is_lin = (op == OP_LIN && lin_unit) || selb;
   const bool is_acc = op == OP_LIN && !lin_unit;
   if (hdr & H_MUL) {

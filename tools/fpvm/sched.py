@@ -38,6 +38,12 @@ BANK_PASSES = int(os.environ.get("OVH_BANK_PASSES", "3"))
 # negations (r02aj: 1,013k -> 1,031-1,038k verifs/s). OVH_GEN_UNITLIN=1 with an interpreter
 # built with OVH_VM_UNIT_LIN restores the unit-sign path (A/B builds).
 ALL_ACC = os.environ.get("OVH_GEN_UNITLIN", "0") != "1"
+# r03: per phase -- a linear phase whose lin ops are all unit sums (or k x a unit sum) runs the
+# cheaper unit block (add chains + one small-scalar reduction, fpvm.hpp lin_sum / scale_reduce),
+# any other linear phase runs every lin op in the general block (unit sums encoded with the
+# FORCE_ACC bit). 0 restores ALL_ACC's one-block-per-phase rule in every phase.
+PHASE_UNIT = os.environ.get("OVH_GEN_PHASE_UNIT", "1") == "1"
+FORCE_ACC = 1 << 24   # w3 bit: run this lin op in the general-coefficient block
 R_MONT = pow(2, 384, P)
 
 
@@ -402,9 +408,10 @@ def words_per_lane(prog):
     return 4
 
 
-def lane_operands(prog, i):
+def lane_operands(prog, i, unit=False):
     """(A, B, C, D, coefs, scale) of op i as the interpreter reads them (value ids or None:
-    None is the zero constant; C of sgn0 / lex / eq / inv is a fixed constant, see encode)."""
+    None is the zero constant; C of sgn0 / lex / eq / inv is a fixed constant, see encode).
+    unit: a unit / scaled lin keeps its scale for the unit block (else coefficients x scale)."""
     ops = prog.ops
     LW = prog.lin_width
     op = ops[i]
@@ -424,7 +431,7 @@ def lane_operands(prog, i):
             coefs = [c for c, _ in u]
             if form[0] == "scaled":
                 scale = form[1]
-                if ALL_ACC:
+                if ALL_ACC and not unit:
                     coefs = [c * scale for c in coefs]
                     scale = 0
         A, B, C, D = srcs[:4]
@@ -476,6 +483,9 @@ def encode(sc):
     for r in sc.rounds:
         lanes = list(r) + [None] * (sc.W - len(r))
         first = len(words)
+        # unit block for this phase's lin ops only when every one of them is a unit sum
+        unit = PHASE_UNIT and ALL_ACC and all(
+            lin_form(sc.prog._lin_terms(ops[i]), LW)[0] in ("unit", "scaled") for i in r if ops[i].kind == "lin")
         for i in lanes:
             if i is None:
                 # an idle lane loads the operands of lane 0 (same addresses: an LDS broadcast,
@@ -484,7 +494,7 @@ def encode(sc):
                 continue
             op = ops[i]
             k = op.kind
-            A, B, C, D, coefs, scale = lane_operands(sc.prog, i)
+            A, B, C, D, coefs, scale = lane_operands(sc.prog, i, unit)
             dst = sc.slot_of.get(i, 0)
             w0 = OPC[k] | dst << 5 | (op.imm & 63) << 16
             if k in ("sgn0", "lex", "eq"):
@@ -494,6 +504,8 @@ def encode(sc):
             else:
                 cref = _operand(sc, C)
             w3 = _c5(coefs[0]) | _c5(coefs[1]) << 5 | _c5(coefs[2]) << 10 | _c5(coefs[3]) << 15 | scale << 20
+            if k == "lin" and not unit and ALL_ACC:
+                w3 |= FORCE_ACC
             words += [w0, _operand(sc, A) | _operand(sc, B) << 16, cref | _operand(sc, D) << 16, w3]
         # the phase header (wave-uniform code paths) in bits 22.. of every lane's w0
         base = len(words) - sc.W * nw
@@ -520,7 +532,8 @@ def phase_bits(w):
     if opc == OPC["selb"]:
         return H_LIN | H_SELB
     if opc == OPC["lin"]:
-        if ca == 1 and all(-1 <= c <= 1 for c in (cb, cc, cd)) and not ALL_ACC:
+        if ca == 1 and all(-1 <= c <= 1 for c in (cb, cc, cd)) and not (w[3] & FORCE_ACC) and \
+                (not ALL_ACC or PHASE_UNIT):
             return H_LIN | (H_LINNEG if min(cb, cc, cd) < 0 else 0)
         return H_ACC
     return H_RARE

@@ -1,5 +1,5 @@
-// Montgomery product on 14 x 28-bit limbs (product scanning, one 64-bit accumulator, no carry
-// word) against the production 12 x 32-bit product (csrc/bls/fp_mul_gfx950.hpp): same interface
+// Montgomery product on 14 x 28-bit limbs (product scanning, 64-bit accumulators, no carry
+// word; one-chain and two-accumulator issue orders, tools/gen_fpmul28.py) against the production 12 x 32-bit product (csrc/bls/fp_mul_gfx950.hpp): same interface
 // (12 x 32-bit limbs in and out, a, b < 4p, result < 1.63p), bit-checked against each other mod p
 // and timed as dependent product chains at 1 and 4 waves per SIMD.
 //   hipcc -O3 --offload-arch=gfx950 -o tools/ubench/fp_mul28 tools/ubench/fp_mul28.hip
@@ -36,8 +36,8 @@ __global__ __launch_bounds__(64) void k_chain(uint32_t iters, uint32_t* out) {
   }
   for (uint32_t i = 0; i < iters; ++i) {
     if (V == 0) fp_mul(x, x, y);
-    else if (V == 1) fp_mul28(x.v, x.v, y.v);
-    else fp_mul28_gfx950(x.v, x.v, y.v);
+    else if (V == 1) fp_mul28_gfx950_1acc(x.v, x.v, y.v);
+    else fp_mul28_gfx950_2acc(x.v, x.v, y.v);
   }
   Fp c;
   vm_canon(c, x);
@@ -70,8 +70,8 @@ int main() {
       if (v)
         for (size_t i = 0; i < (size_t)grid * 64 * 12; ++i) bad[v] += h0[i] != h1[i];
     }
-    printf("{\"waves\": %d, \"ns_per_mul_32x12\": %.1f, \"ns_per_mul_28x14_cpp\": %.1f, \"ns_per_mul_28x14_asm\": "
-           "%.1f, \"speedup_cpp\": %.3f, \"speedup_asm\": %.3f, \"mismatched_words\": [%zu, %zu]}\n",
+    printf("{\"waves\": %d, \"ns_per_mul_32x12\": %.1f, \"ns_per_mul_28x14_1acc\": %.1f, \"ns_per_mul_28x14_2acc\": "
+           "%.1f, \"speedup_1acc\": %.3f, \"speedup_2acc\": %.3f, \"mismatched_words\": [%zu, %zu]}\n",
            grid, t[0] * 1e6 / iters, t[1] * 1e6 / iters, t[2] * 1e6 / iters, t[0] / t[1], t[0] / t[2], bad[1], bad[2]);
   }
   return 0;
