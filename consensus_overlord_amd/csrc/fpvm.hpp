@@ -82,8 +82,9 @@ VM_FN void unpack4(Fp& r, int q, const u32x4 v) {
 
 VM_FN void ld_slots4(Fp& A, Fp& B, Fp& C, Fp& D, const uint32_t* __restrict__ slots,
                      const uint32_t* __restrict__ cst, uint32_t ra, uint32_t rb, uint32_t rc, uint32_t rd) {
-#if defined(__HIPCC__) && !defined(OVH_VM_CC_LOADS)
-  // The twelve reads are issued in one asm statement and waited for in three (one per limb
+#if defined(__HIPCC__) && defined(OVH_VM_ASM_LOADS)
+  // (A/B build; the compiler-scheduled loads below measured 1.3% faster in the vote kernel,
+  // profiles/r03g_ab_summary.txt.) The twelve reads are issued in one asm statement and waited for in three (one per limb
   // quarter), so the compiler's waitcnt pass sees no LDS loads here: left to it, the loop's back
   // edge merged these loads' pending state with the stores the phase ends with and it put an
   // lgkmcnt(0) before the next phase's reads -- a full LDS round trip for the stores, every phase.

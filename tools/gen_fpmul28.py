@@ -126,13 +126,15 @@ def main():
         lines, clob = fn()
         n[name] = len(lines)
         emit_fn(e, name, lines, clob)
-    e("#if defined(OVH_FPMUL28_1ACC)")
+    e("// one-chain order by default: the two-accumulator order measured 1.5% slower in the vote kernel")
+    e("// (profiles/r03g_ab_summary.txt) and 5% slower at 4 waves per SIMD (r03g fp_mul28 ubench)")
+    e("#if defined(OVH_FPMUL28_2ACC)")
     e("__device__ __forceinline__ void fp_mul28_gfx950(uint32_t* r, const uint32_t* a, const uint32_t* b) {")
-    e("  fp_mul28_gfx950_1acc(r, a, b);")
+    e("  fp_mul28_gfx950_2acc(r, a, b);")
     e("}")
     e("#else")
     e("__device__ __forceinline__ void fp_mul28_gfx950(uint32_t* r, const uint32_t* a, const uint32_t* b) {")
-    e("  fp_mul28_gfx950_2acc(r, a, b);")
+    e("  fp_mul28_gfx950_1acc(r, a, b);")
     e("}")
     e("#endif")
     e("}  // namespace ovh")
