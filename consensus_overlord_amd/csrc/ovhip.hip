@@ -290,9 +290,10 @@ __device__ __forceinline__ void fold_unit(uint32_t t, uint32_t m, const VmDev& p
 // The vote waves of a CU run the same program in near lockstep, so every phase's operand loads
 // (12 KB per wave) reach the CU's LDS at the same moment. OVH_VOTE_STAGGER > 0 offsets the start
 // of the wave on SIMD s by s x OVH_VOTE_STAGGER x 64 cycles (the offset persists: every wave's
-// phases take equally long), spreading those bursts.
+// phases take equally long), spreading those bursts. r03k A/B: 6 / 12 / 24 each +0.8-1.2%
+// verifs/s against 0 (profiles/r03k_stagger_ab.txt); 12 is the default.
 #ifndef OVH_VOTE_STAGGER
-#define OVH_VOTE_STAGGER 0
+#define OVH_VOTE_STAGGER 12
 #endif
 __device__ __forceinline__ void vote_stagger() {
 #if OVH_VOTE_STAGGER > 0
