@@ -219,6 +219,11 @@ struct VmDev {  // a program in device memory
   uint64_t* trace;  // OVH_FLAG_VM_TRACE: nphases + 1 timestamps of workgroup 0, else null
 };
 
+// Batches of at most SMALL_MAX votes (one vote per wave: 1,024 waves fill the chip's SIMDs)
+// take the small-batch path: votew per vote, fold, one final exponentiation (verify_small_locked).
+#ifndef SMALL_MAX
+#define SMALL_MAX 1024u
+#endif
 #define VM_SLICES 4  // 16-lane slices per 64-lane workgroup (vote, vote_t)
 // LDS layout of the VM kernels (words): the constant table, then slot regions that start on a
 // 128-byte boundary and repeat at 128-byte strides, so slot s and constant c share LDS banks
@@ -520,32 +525,37 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
 // f = Miller(pk, H) Miller(-G1, sigma) as one two-pair Miller loop, stored to the F planes of
 // element 0, and the code (precedence as k_vm_vote / k_vm_vote_t); k_vm_final1 then checks
 // FE(f) == 1. No MSM, no fold, no bisection: the vote's own pairing equation is the check.
+// One vote on a whole 64-lane wave (vote1 / vote_t1 and votew / votew_t: the two pairs share
+// input and output layouts): inputs of vote i (pk bytes or table entry e, signature bytes, the u
+// planes of slab index i), the program with RLC scalar `scalar` (its `st` ops write the f
+// planes of slab index i), then the per-vote code in k_vm_vote's precedence.
+static_assert(VM_VOTEW_NIN == VM_VOTE1_NIN && VM_VOTEW_T_NIN == VM_VOTE_T1_NIN && VM_VOTEW_W == 64 &&
+                  VM_VOTEW_T_W == 64 && VM_VOTE1_W == 64 && VM_VOTE_T1_W == 64,
+              "one-vote-per-wave programs share the vote1 / vote_t1 layouts");
 template <bool TABLE>
-__global__ __launch_bounds__(64) void k_vm_vote1(VmDev prog, const uint32_t* __restrict__ cst_g,
-                                                 const uint8_t* __restrict__ pk_bytes, PkSrc pk,
-                                                 const uint8_t* __restrict__ sig, Slab s, int32_t* __restrict__ code) {
+__device__ __forceinline__ void vote_wave(const VmDev& prog, uint32_t nph, uint32_t ns, const uint16_t* IN,
+                                          const uint16_t* OUT, const uint32_t* __restrict__ cst_g,
+                                          const uint8_t* __restrict__ pk_bytes, PkSrc pk, uint32_t e,
+                                          const uint8_t* __restrict__ sig, Slab s, uint32_t i, uint64_t scalar,
+                                          int32_t* __restrict__ code) {
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
   uint32_t* slots = lds + SLOT_BASE_W;
-  constexpr uint32_t NS = TABLE ? VM_VOTE_T1_NSLOTS : VM_VOTE1_NSLOTS;
-  constexpr uint32_t NPH = TABLE ? VM_VOTE_T1_NPHASES : VM_VOTE1_NPHASES;
-  static_assert(VM_VOTE1_W == 64 && VM_VOTE_T1_W == 64, "standalone vote programs take a whole wave");
-  uint32_t* hdr = slots + NS * 12;  // [sig flags, pk flags]
+  uint32_t* hdr = slots + ns * 12;  // [sig flags, pk flags]
   const uint32_t lane = threadIdx.x;
   load_consts(cst, cst_g, VM_NCONST);
-  const uint32_t e = TABLE && pk.idx ? (uint32_t)pk.idx[0] : 0u;
   if (lane == 0) {
     uint32_t x1[12], x0[12], bad, inf, sort, xz;
     parse_hdr(sig, 96, x1, x0, bad, inf, sort, xz);
     if constexpr (TABLE) {
-      slot_put(slots, VM_VOTE_T1_IN[VM_VOTE_T1_IN_SIG_X1], x1);
-      slot_put(slots, VM_VOTE_T1_IN[VM_VOTE_T1_IN_SIG_X0], x0);
-      slot_flag(slots, VM_VOTE_T1_IN[VM_VOTE_T1_IN_SIG_SORT], sort);
+      slot_put(slots, IN[VM_VOTE_T1_IN_SIG_X1], x1);
+      slot_put(slots, IN[VM_VOTE_T1_IN_SIG_X0], x0);
+      slot_flag(slots, IN[VM_VOTE_T1_IN_SIG_SORT], sort);
     } else {
-      slot_put(slots, VM_VOTE1_IN[VM_VOTE1_IN_SIG_X1], x1);
-      slot_put(slots, VM_VOTE1_IN[VM_VOTE1_IN_SIG_X0], x0);
-      slot_flag(slots, VM_VOTE1_IN[VM_VOTE1_IN_SIG_SORT], sort);
+      slot_put(slots, IN[VM_VOTE1_IN_SIG_X1], x1);
+      slot_put(slots, IN[VM_VOTE1_IN_SIG_X0], x0);
+      slot_flag(slots, IN[VM_VOTE1_IN_SIG_SORT], sort);
     }
     hdr[0] = bad | inf << 1 | xz << 2;
   } else if (lane == 1) {
@@ -554,36 +564,36 @@ __global__ __launch_bounds__(64) void k_vm_vote1(VmDev prog, const uint32_t* __r
     } else {
       uint32_t x[12], bad, inf, sort, xz;
       parse_hdr(pk_bytes, 48, x, x, bad, inf, sort, xz);
-      slot_put(slots, VM_VOTE1_IN[VM_VOTE1_IN_PK_X], x);
-      slot_flag(slots, VM_VOTE1_IN[VM_VOTE1_IN_PK_SORT], sort);
+      slot_put(slots, IN[VM_VOTE1_IN_PK_X], x);
+      slot_flag(slots, IN[VM_VOTE1_IN_PK_SORT], sort);
       hdr[1] = bad | inf << 1 | xz << 2;
     }
   } else if (lane >= 2 && lane < 6) {
     Fp u;
-    s.ld(u, S_U + (lane - 2), 0);
-    if constexpr (TABLE) slot_put(slots, VM_VOTE_T1_IN[VM_VOTE_T1_IN_U00 + (lane - 2)], u.v);
-    else slot_put(slots, VM_VOTE1_IN[VM_VOTE1_IN_U00 + (lane - 2)], u.v);
+    s.ld(u, S_U + (lane - 2), i);
+    if constexpr (TABLE) slot_put(slots, IN[VM_VOTE_T1_IN_U00 + (lane - 2)], u.v);
+    else slot_put(slots, IN[VM_VOTE1_IN_U00 + (lane - 2)], u.v);
   } else if (TABLE && lane >= 6 && lane < 9) {
     Fp v;
     Slab{const_cast<uint32_t*>(pk.planes), pk.cap}.ld(v, lane - 6, e);
-    if constexpr (TABLE) slot_put(slots, VM_VOTE_T1_IN[VM_VOTE_T1_IN_PK_X + (lane - 6)], v.v);
+    if constexpr (TABLE) slot_put(slots, IN[VM_VOTE_T1_IN_PK_X + (lane - 6)], v.v);
   }
   __syncthreads();
-  vm::run(prog.code, NPH, 64, lane, true, slots, cst, 1, vm::Out{s.p, s.cap, 0});
+  vm::run(prog.code, nph, 64, lane, true, slots, cst, scalar, vm::Out{s.p, s.cap, i});
   if (lane == 0) {
     const uint32_t sf = hdr[0], pf = hdr[1];
     const uint32_t sg_bad = sf & 1, sg_inf = (sf >> 1) & 1, sg_xz = (sf >> 2) & 1;
     uint32_t sg_ok, sg_grp, h_inf, pk_ok = 1, pk_grp = 1;
     if constexpr (TABLE) {
-      sg_ok = slot_flag_get(slots, VM_VOTE_T1_OUT[VM_VOTE_T1_OUT_SIG_OK]);
-      sg_grp = slot_flag_get(slots, VM_VOTE_T1_OUT[VM_VOTE_T1_OUT_SIG_GRP]);
-      h_inf = slot_flag_get(slots, VM_VOTE_T1_OUT[VM_VOTE_T1_OUT_H_INF]);
+      sg_ok = slot_flag_get(slots, OUT[VM_VOTE_T1_OUT_SIG_OK]);
+      sg_grp = slot_flag_get(slots, OUT[VM_VOTE_T1_OUT_SIG_GRP]);
+      h_inf = slot_flag_get(slots, OUT[VM_VOTE_T1_OUT_H_INF]);
     } else {
-      pk_ok = slot_flag_get(slots, VM_VOTE1_OUT[VM_VOTE1_OUT_PK_OK]);
-      pk_grp = slot_flag_get(slots, VM_VOTE1_OUT[VM_VOTE1_OUT_PK_GRP]);
-      sg_ok = slot_flag_get(slots, VM_VOTE1_OUT[VM_VOTE1_OUT_SIG_OK]);
-      sg_grp = slot_flag_get(slots, VM_VOTE1_OUT[VM_VOTE1_OUT_SIG_GRP]);
-      h_inf = slot_flag_get(slots, VM_VOTE1_OUT[VM_VOTE1_OUT_H_INF]);
+      pk_ok = slot_flag_get(slots, OUT[VM_VOTE1_OUT_PK_OK]);
+      pk_grp = slot_flag_get(slots, OUT[VM_VOTE1_OUT_PK_GRP]);
+      sg_ok = slot_flag_get(slots, OUT[VM_VOTE1_OUT_SIG_OK]);
+      sg_grp = slot_flag_get(slots, OUT[VM_VOTE1_OUT_SIG_GRP]);
+      h_inf = slot_flag_get(slots, OUT[VM_VOTE1_OUT_H_INF]);
     }
     // key flags in the table's terms, then the precedence of k_vm_vote_t (consensus.rs:397-416)
     uint32_t kf = pf;
@@ -604,14 +614,42 @@ __global__ __launch_bounds__(64) void k_vm_vote1(VmDev prog, const uint32_t* __r
   }
 }
 
-// FE(f) == 1 for the standalone vote (skipped when its code is already an error): *verdict,
-// and code BLST_VERIFY_FAIL when the pairing check fails.
-__global__ __launch_bounds__(64) void k_vm_final1(VmDev prog, const uint32_t* __restrict__ cst_g, Slab F,
-                                                  int32_t* __restrict__ code, int32_t* __restrict__ verdict) {
-  if (*code != 0) {
-    if (threadIdx.x == 0) *verdict = 0;
-    return;
-  }
+// The standalone vote (ovh_verify, one-QC checks): vote1 / vote_t1 at slab index 0, no
+// coefficient.
+template <bool TABLE>
+__global__ __launch_bounds__(64) void k_vm_vote1(VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                 const uint8_t* __restrict__ pk_bytes, PkSrc pk,
+                                                 const uint8_t* __restrict__ sig, Slab s, int32_t* __restrict__ code) {
+  const uint32_t e = TABLE && pk.idx ? (uint32_t)pk.idx[0] : 0u;
+  if constexpr (TABLE)
+    vote_wave<true>(prog, VM_VOTE_T1_NPHASES, VM_VOTE_T1_NSLOTS, VM_VOTE_T1_IN, VM_VOTE_T1_OUT, cst_g, pk_bytes, pk, e,
+                    sig, s, 0, 1, code);
+  else
+    vote_wave<false>(prog, VM_VOTE1_NPHASES, VM_VOTE1_NSLOTS, VM_VOTE1_IN, VM_VOTE1_OUT, cst_g, pk_bytes, pk, e, sig,
+                     s, 0, 1, code);
+}
+
+// Small batches (n <= SMALL_MAX, verify_small_locked): vote i = workgroup i on a whole wave,
+// program votew / votew_t with the vote's RLC coefficient: f_i = Miller(r pk, H) Miller(-G1,
+// r sigma) to the slab's f planes, code to codes[i].
+template <bool TABLE>
+__global__ __launch_bounds__(64) void k_vm_votew(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                 const uint8_t* __restrict__ pks, PkSrc pk,
+                                                 const uint8_t* __restrict__ sigs, Slab s, uint64_t seed,
+                                                 uint64_t base, int32_t* __restrict__ codes) {
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  const uint32_t e = TABLE ? (pk.idx ? (uint32_t)pk.idx[i] : i) : 0u;
+  if constexpr (TABLE)
+    vote_wave<true>(prog, VM_VOTEW_T_NPHASES, VM_VOTEW_T_NSLOTS, VM_VOTEW_T_IN, VM_VOTEW_T_OUT, cst_g, nullptr, pk, e,
+                    sigs + (size_t)i * 96, s, i, vote_scalar(seed, base, i), codes + i);
+  else
+    vote_wave<false>(prog, VM_VOTEW_NPHASES, VM_VOTEW_NSLOTS, VM_VOTEW_IN, VM_VOTEW_OUT, cst_g, pks + (size_t)i * 48,
+                     pk, e, sigs + (size_t)i * 96, s, i, vote_scalar(seed, base, i), codes + i);
+}
+
+// FE(F_u) == 1 for unit u of the F planes (program final1): the shared body of the FE kernels.
+__device__ __forceinline__ bool fe_one(const VmDev& prog, const uint32_t* __restrict__ cst_g, Slab F, uint32_t u) {
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -620,13 +658,43 @@ __global__ __launch_bounds__(64) void k_vm_final1(VmDev prog, const uint32_t* __
   load_consts(cst, cst_g, VM_NCONST);
   if (lane < 12) {
     Fp v;
-    F.ld(v, lane, 0);
+    F.ld(v, lane, u);
     slot_put(slots, VM_FINAL1_IN[lane], v.v);
   }
   __syncthreads();
   vm::run(prog.code, VM_FINAL1_NPHASES, VM_FINAL1_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
-  if (lane == 0) {
-    const bool ok = slot_flag_get(slots, VM_FINAL1_OUT[0]) != 0;
+  return slot_flag_get(slots, VM_FINAL1_OUT[0]) != 0;
+}
+
+// A small batch's combined check: FE(prod f_i) == 1 on the folded partial (unit 0) -> *verdict.
+__global__ __launch_bounds__(64) void k_vm_fe(VmDev prog, const uint32_t* __restrict__ cst_g, Slab F,
+                                              int32_t* __restrict__ verdict) {
+  const bool ok = fe_one(prog, cst_g, F, 0);
+  if (threadIdx.x == 0) *verdict = ok ? 1 : 0;
+}
+
+// A small batch's bisection (skipped when *verdict == 1): every vote with code 0 on its own,
+// FE(f_i) = (e(pk, H) / e(G1, sigma))^r == 1 exactly when the vote verifies (r != 0 mod the
+// group order).
+__global__ __launch_bounds__(64) void k_vm_votefe(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g, Slab s,
+                                                  int32_t* __restrict__ codes, const int32_t* __restrict__ verdict) {
+  if (*verdict == 1) return;
+  const uint32_t i = blockIdx.x;
+  if (i >= n || codes[i] != 0) return;
+  const bool ok = fe_one(prog, cst_g, Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, i);
+  if (threadIdx.x == 0) codes[i] = ok ? 0 : BLST_VERIFY_FAIL;
+}
+
+// FE(f) == 1 for the standalone vote (skipped when its code is already an error): *verdict,
+// and code BLST_VERIFY_FAIL when the pairing check fails.
+__global__ __launch_bounds__(64) void k_vm_final1(VmDev prog, const uint32_t* __restrict__ cst_g, Slab F,
+                                                  int32_t* __restrict__ code, int32_t* __restrict__ verdict) {
+  if (*code != 0) {
+    if (threadIdx.x == 0) *verdict = 0;
+    return;
+  }
+  const bool ok = fe_one(prog, cst_g, F, 0);
+  if (threadIdx.x == 0) {
     *verdict = ok ? 1 : 0;
     if (!ok) *code = BLST_VERIFY_FAIL;
   }
@@ -1275,6 +1343,9 @@ struct ovh_ctx {
   // pipeline placement (environment OVH_FOLD_SIDE, read at ovh_create): 1 (default) runs the
   // fold levels on the final stream instead of between two vote kernels on the main stream
   bool fold_side = true;
+  // batches of 2 .. small_max votes checked alone run the small-batch path (verify_small_locked);
+  // OVH_SMALL_MAX=0 turns it off (A/B builds and tests of the standard path)
+  uint32_t small_max = SMALL_MAX;
   XmdTemplates xmd;
   std::mutex mu;  // Crypto is Send + Sync: every entry point holds it for its whole call
   uint32_t cap = 0, red_cap = 0;
@@ -1322,7 +1393,8 @@ struct ovh_ctx {
   uint64_t hb_k = 0;
   // Fp-VM programs + constant table in device memory
   VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{},
-      vm_pkchk{}, vm_g1padd{}, vm_sign0{}, vm_sign1{}, vm_vote1{}, vm_vote_t1{}, vm_final1{};
+      vm_pkchk{}, vm_g1padd{}, vm_sign0{}, vm_sign1{}, vm_vote1{}, vm_vote_t1{}, vm_final1{}, vm_votew{},
+      vm_votew_t{};
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
@@ -1364,6 +1436,8 @@ static_assert(VM_MADD_W == VM_PADD_W && VM_HDBL1_W == VM_HDBL2_W && VM_HDBL1_W =
 static constexpr size_t LDS_SIGCHK = ((size_t)SLOT_BASE_W + (64 / VM_SIGCHK_W) * (size_t)SIGCHK_STRIDE_W) * 4;
 static constexpr uint32_t VOTE1_NSLOTS = VM_VOTE1_NSLOTS > VM_VOTE_T1_NSLOTS ? VM_VOTE1_NSLOTS : VM_VOTE_T1_NSLOTS;
 static constexpr size_t LDS_VOTE1 = ((size_t)SLOT_BASE_W + VOTE1_NSLOTS * 12 + 4) * 4;
+static constexpr uint32_t VOTEW_NSLOTS = VM_VOTEW_NSLOTS > VM_VOTEW_T_NSLOTS ? VM_VOTEW_NSLOTS : VM_VOTEW_T_NSLOTS;
+static constexpr size_t LDS_VOTEW = ((size_t)SLOT_BASE_W + VOTEW_NSLOTS * 12 + 4) * 4;
 static constexpr size_t LDS_FINAL1 = ((size_t)SLOT_BASE_W + (size_t)VM_FINAL1_NSLOTS * 12) * 4;
 static constexpr size_t LDS_SIGN = ((size_t)SLOT_BASE_W + (64 / VM_SIGN0_W) * (size_t)SIGN_STRIDE_W) * 4;
 static constexpr size_t LDS_PKCHK = ((size_t)SLOT_BASE_W + (64 / VM_PKCHK_W) * (size_t)PKCHK_STRIDE_W) * 4;
@@ -1371,7 +1445,7 @@ static constexpr uint32_t G1PADD_STRIDE_W = align128w(VM_G1PADD_NSLOTS * 12);
 static constexpr size_t LDS_G1PADD = ((size_t)SLOT_BASE_W + (64 / VM_G1PADD_W) * (size_t)G1PADD_STRIDE_W) * 4;
 static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024 && LDS_SIGCHK <= 64 * 1024 &&
                   LDS_PKCHK <= 64 * 1024 && LDS_G1PADD <= 64 * 1024 && LDS_SIGN <= 64 * 1024 &&
-                  LDS_VOTE1 <= 64 * 1024 && LDS_FINAL1 <= 64 * 1024 && VM_G1PADD_NIN == 6,
+                  LDS_VOTE1 <= 64 * 1024 && LDS_FINAL1 <= 64 * 1024 && LDS_VOTEW <= 64 * 1024 && VM_G1PADD_NIN == 6,
               "default LDS limit");
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
@@ -1432,6 +1506,10 @@ static int vm_init(ovh_ctx* c) {
                 VM_VOTE1_OUT, VM_VOTE1_NOUT));
   CHK(vm_upload(c, c->vm_vote_t1, VM_VOTE_T1_CODE, VM_VOTE_T1_NPHASES, VM_VOTE_T1_W, VM_VOTE_T1_NW, VM_VOTE_T1_IN,
                 VM_VOTE_T1_NIN, VM_VOTE_T1_OUT, VM_VOTE_T1_NOUT));
+  CHK(vm_upload(c, c->vm_votew, VM_VOTEW_CODE, VM_VOTEW_NPHASES, VM_VOTEW_W, VM_VOTEW_NW, VM_VOTEW_IN, VM_VOTEW_NIN,
+                VM_VOTEW_OUT, VM_VOTEW_NOUT));
+  CHK(vm_upload(c, c->vm_votew_t, VM_VOTEW_T_CODE, VM_VOTEW_T_NPHASES, VM_VOTEW_T_W, VM_VOTEW_T_NW, VM_VOTEW_T_IN,
+                VM_VOTEW_T_NIN, VM_VOTEW_T_OUT, VM_VOTEW_T_NOUT));
   CHK(vm_upload(c, c->vm_final1, VM_FINAL1_CODE, VM_FINAL1_NPHASES, VM_FINAL1_W, VM_FINAL1_NW, VM_FINAL1_IN,
                 VM_FINAL1_NIN, VM_FINAL1_OUT, VM_FINAL1_NOUT));
   CHK(vm_upload(c, c->vm_sign0, VM_SIGN0_CODE, VM_SIGN0_NPHASES, VM_SIGN0_W, VM_SIGN0_NW, VM_SIGN0_IN, VM_SIGN0_NIN,
@@ -1831,9 +1909,68 @@ static int verify_one_locked(ovh_ctx* c, const uint8_t* d_sig, const uint8_t* d_
   return 0;
 }
 
+// A small batch checked alone (2 <= n <= c->small_max): hash_to_field and
+// k_vm_votew (one vote per wave: its checks, H(m), r pk, r sigma and f_i = Miller(r pk, H)
+// Miller(-G1, r sigma)) on the main stream; on the slot's final stream the fold of the f_i of
+// the votes with code 0 down to one partial, FE(prod f_i) == 1 (k_vm_fe) and, when that fails,
+// FE(f_i) == 1 per vote (k_vm_votefe). No MSM, no Miller loop in the final: one final
+// exponentiation per batch. Caller holds c->mu.
+static int verify_small_locked(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
+                               int32_t* d_codes) {
+  int slot;
+  CHK(take_slot(c, &slot));
+  Slab s{c->state_slot[slot], c->cap};
+  hipStream_t st = c->stream;
+  c->ev_mask = 0;
+  uint64_t seed, base;
+  CHK(draw_seed(c, &seed, &base));
+  c->slot_seed[slot] = seed;
+  c->slot_base[slot] = base;
+  {
+    StageScope p(c, ST_H2F);
+    k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s);
+  }
+  {
+    StageScope p(c, ST_VOTE);
+    if (key.bytes)
+      k_vm_votew<false><<<n, 64, LDS_VOTEW, st>>>(n, c->vm_votew, c->vm_consts, key.bytes, PkSrc{}, d_sigs, s, seed,
+                                                  base, d_codes);
+    else
+      k_vm_votew<true><<<n, 64, LDS_VOTEW, st>>>(n, c->vm_votew_t, c->vm_consts, nullptr, key.pts, d_sigs, s, seed,
+                                                 base, d_codes);
+  }
+  hipStream_t fst = c->fs[slot];
+  HIPCHK(hipEventRecord(c->ev_front[slot], st));
+  HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
+  int reg = 0;
+  uint32_t m = (n + 3) / 4;
+  {
+    StageScope p(c, ST_FOLD, fst);
+    k_vm_fold<VM_FOLD_UNITS><<<(m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, fst>>>(
+        n, c->vm_fold, c->vm_consts, Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{nullptr, 0},
+        region_F(c, slot, 0), d_codes);
+  }
+  CHK(fold_down(c, slot, fst, VM_SLICES, &reg, &m, 1));
+  int32_t* verdict = c->result + RES_BATCH + slot;
+  {
+    StageScope p(c, ST_FINAL, fst);
+    k_vm_fe<<<1, 64, LDS_FINAL1, fst>>>(c->vm_final1, c->vm_consts, region_F(c, slot, reg), verdict);
+  }
+  {
+    StageScope p(c, ST_FALLBACK, fst);
+    k_vm_votefe<<<n, 64, LDS_FINAL1, fst>>>(n, c->vm_final1, c->vm_consts, s, d_codes, verdict);
+  }
+  HIPCHK(hipEventRecord(c->ev_back[slot], fst));
+  HIPCHK(hipGetLastError());
+  c->slot_n[slot] = n;
+  c->last_n = 0;  // no (f, r sigma) state for ovh_batch_partial_device / the standard bisection
+  return 0;
+}
+
 static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
                                int32_t* d_codes, bool pipe = false) {
   CHK(ensure_cap(c, n));
+  if (n >= 2 && n <= c->small_max) return verify_small_locked(c, (uint32_t)n, d_sigs, d_hashes, key, d_codes);
   int slot;
   CHK(take_slot(c, &slot));
   const bool side = c->fold_side;
@@ -2378,6 +2515,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   c->device = device;
   c->flags = flags;
   if (const char* e = getenv("OVH_FOLD_SIDE")) c->fold_side = atoi(e) != 0;
+  if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->wg_cap = 4u * (uint32_t)ncu;

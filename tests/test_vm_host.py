@@ -207,7 +207,8 @@ def test_fp_inv(hx):
 def test_percall_programs_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
     """The per-call programs through the interpreter == simulator: sigchk / pkchk on golden
     signatures and keys (a non-subgroup case included), g1padd, sign0 + sign1 over a golden
-    key's scalar chunks, and vote1 / vote_t1 + final1 on a golden vote (gen.check ties each to
+    key's scalar chunks, vote1 / vote_t1 + final1 and the small-batch votew / votew_t + final1 on a
+    golden vote (gen.check ties each to
     the oracle: decompressed points, sums, the golden signature, the pairing verdict)."""
     consts, progs_ = built
     bls = gen._oracle()
@@ -236,3 +237,8 @@ def test_percall_programs_on_interpreter(hx, built, golden_votes, any_all):  # n
     tin = {n: inp[n] for n in ("sig_x0", "sig_x1", "sig_sort", "u00", "u01", "u10", "u11")}
     tin.update(pk_X=pk[0] * 5 % P, pk_Y=pk[1] * 5 % P, pk_Z=5)
     run("vote_t1", tin, 1)
+    # the small-batch programs under a random RLC scalar: FE(f) == 1 for the valid golden vote
+    r = 0x9E3779B97F4A7C15
+    o = run("votew", inp, r)
+    assert run("final1", {"f%d" % j: o["st:f%d" % j] for j in range(12)}) == {"ok": 1}
+    run("votew_t", tin, r)

@@ -179,6 +179,46 @@ def build_vote1(table: bool):
     return build
 
 
+def build_votew(table: bool):
+    """votew / votew_t: one vote of a small batch (n <= 1024, ovhip.hip k_vm_votew) on a whole
+    64-lane wave: the vote's checks and H(m) as in vote1 / vote_t1, the RLC products r pk
+    (projective, [a] pk + [b] phi(pk)) and r sigma ([a] sigma + [b] tau, the rs chain), and
+    f = Miller(r pk, H) Miller(-G1, r sigma), so that FE(f) = (e(pk, H) / e(G1, sigma))^r: the
+    batch's combined check is FE(prod f_i) == 1 with no MSM and no Miller loop in the final, and a
+    vote's own check is FE(f_i) == 1. The sigma side (decompression, r sigma, its Miller loop)
+    runs beside hash_to_G2 on the wave's idle lanes."""
+    def build():
+        p = Prog("votew_t" if table else "votew")
+        a = Alg(p, use_sop=USE_SOP, fast_sqrt=True)
+        R = p.const(R_MONT)
+        if table:
+            Pp = (p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z"))
+        else:
+            pk_ok, (px, py) = a.g1_decompress(p.input("pk_x") * R, p.input("pk_sort"))
+            Pp = (px, py, p.one)
+            pk_grp, _ = a.g1_in_group(Pp)
+        sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
+        u0 = (p.input("u00"), p.input("u01"))
+        u1 = (p.input("u10"), p.input("u11"))
+        p.section = "sig"
+        sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
+        Qs = (qx, qy, (p.one, p.zero))
+        sig_grp = a.g2_in_group(Qs)
+        rS = a.pt_mul_glv("f2", Qs, a.g2_neg_psi2(Qs))
+        p.section = None
+        H = a.hash_to_g2(u0, u1)
+        h_inf = a.f2_is_zero(H[2])
+        rP = a.pt_mul_glv("fp", Pp, a.g1_phi(Pp))
+        f = a.f12_mul(a.miller_loop_multi([(rP, H)]), a.miller_loop_multi([((p.const(G1X), p.const(-G1Y)), rS)]))
+        flags = [sig_ok, sig_grp, h_inf] if table else [pk_ok, pk_grp, sig_ok, sig_grp, h_inf]
+        for name, v in zip(VOTE_T_OUT if table else VOTE_OUT, flags):
+            p.output(name, v)
+        for (name, plane), v in zip(VOTE1_ST, flat12(f)):
+            p.store(name, v, plane)
+        return p
+    return build
+
+
 def build_final1():
     p = Prog("final1")
     a = Alg(p, inv_op=True, use_sop=USE_SOP)
@@ -413,6 +453,8 @@ PROGRAMS["pkchk"] = (build_pkchk, PKCHK_IN, PKCHK_OUT)
 PROGRAMS["vote1"] = (build_vote1(False), VOTE_IN, VOTE_OUT)
 PROGRAMS["vote_t1"] = (build_vote1(True), VOTE_T_IN, VOTE_T_OUT)
 PROGRAMS["final1"] = (build_final1, f12_names("f"), ["ok"])
+PROGRAMS["votew"] = (build_votew(False), VOTE_IN, VOTE_OUT)
+PROGRAMS["votew_t"] = (build_votew(True), VOTE_T_IN, VOTE_T_OUT)
 PROGRAMS["sign0"] = (build_sign0, SIGN0_IN, SIGN_ACC + SIGN_H)
 PROGRAMS["sign1"] = (build_sign1, SIGN_ACC + SIGN_H, SIGN_ACC)
 PROGRAMS["g1padd"] = (build_g1padd, G1A_IN + G1B_IN, G1_OUT)
