@@ -648,6 +648,78 @@ __global__ __launch_bounds__(64) void k_vm_votew(uint32_t n, VmDev prog, const u
                      pk, e, sigs + (size_t)i * 96, s, i, vote_scalar(seed, base, i), codes + i);
 }
 
+// verify_aggregated_signature (verify_aggregated_vm), the part without the aggregated key, on a
+// side stream beside the keys' decompression / subgroup checks / tree sum: program qcpre (the
+// signature's checks, H = hash_to_G2, g = Miller(-G1, sigma)) -> H in the S_RS planes and g in
+// the f planes of slab index 0; flags word: signature header flags | sig_ok << 8 | sig_grp << 9
+// | h_inf << 10.
+__global__ __launch_bounds__(64) void k_vm_qcpre(VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                 const uint8_t* __restrict__ sig, Slab s, uint32_t* __restrict__ flags) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  uint32_t* slots = lds + SLOT_BASE_W;
+  uint32_t* hdr = slots + VM_QCPRE_NSLOTS * 12;
+  const uint32_t lane = threadIdx.x;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (lane == 0) {
+    uint32_t x1[12], x0[12], bad, inf, sort, xz;
+    parse_hdr(sig, 96, x1, x0, bad, inf, sort, xz);
+    slot_put(slots, VM_QCPRE_IN[VM_QCPRE_IN_SIG_X1], x1);
+    slot_put(slots, VM_QCPRE_IN[VM_QCPRE_IN_SIG_X0], x0);
+    slot_flag(slots, VM_QCPRE_IN[VM_QCPRE_IN_SIG_SORT], sort);
+    hdr[0] = bad | inf << 1 | xz << 2;
+  } else if (lane >= 2 && lane < 6) {
+    Fp u;
+    s.ld(u, S_U + (lane - 2), 0);
+    slot_put(slots, VM_QCPRE_IN[VM_QCPRE_IN_U00 + (lane - 2)], u.v);
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_QCPRE_NPHASES, VM_QCPRE_W, lane, true, slots, cst, 0, vm::Out{s.p, s.cap, 0});
+  if (lane == 0)
+    *flags = hdr[0] | slot_flag_get(slots, VM_QCPRE_OUT[VM_QCPRE_OUT_SIG_OK]) << 8 |
+             slot_flag_get(slots, VM_QCPRE_OUT[VM_QCPRE_OUT_SIG_GRP]) << 9 |
+             slot_flag_get(slots, VM_QCPRE_OUT[VM_QCPRE_OUT_H_INF]) << 10;
+}
+
+// ... and the rest once the aggregated key (table entry 0 of pk: projective planes + flags) and
+// qcpre are done: program qcmil, f = Miller(apk, H) g -> the f planes of slab index 1, then the
+// code in vote_t1's precedence (consensus.rs:397-416 via verify_aggregated_signature).
+__global__ __launch_bounds__(64) void k_vm_qcmil(VmDev prog, const uint32_t* __restrict__ cst_g, PkSrc pk, Slab s,
+                                                 const uint32_t* __restrict__ flags, int32_t* __restrict__ code) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  uint32_t* slots = lds + SLOT_BASE_W;
+  const uint32_t lane = threadIdx.x;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (lane < 21) {
+    Fp v;
+    if (lane < 3) Slab{const_cast<uint32_t*>(pk.planes), pk.cap}.ld(v, lane, 0);
+    else if (lane < 9) s.ld(v, S_RS + (lane - 3), 0);
+    else s.ld(v, S_F + (lane - 9), 0);
+    slot_put(slots, VM_QCMIL_IN[lane], v.v);
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_QCMIL_NPHASES, VM_QCMIL_W, lane, true, slots, cst, 0, vm::Out{s.p, s.cap, 1});
+  if (lane == 0) {
+    const uint32_t sf = *flags, kf = pk.flags[0];
+    const uint32_t sg_bad = sf & 1, sg_inf = (sf >> 1) & 1, sg_xz = (sf >> 2) & 1;
+    const uint32_t sg_ok = (sf >> 8) & 1, sg_grp = (sf >> 9) & 1, h_inf = (sf >> 10) & 1;
+    int32_t c;
+    if (kf & PKF_PARSE) c = OVH_ERR_PUBKEY;
+    else if (sg_bad) c = BLST_BAD_ENCODING;
+    else if (!sg_inf && !sg_ok) c = BLST_POINT_NOT_ON_CURVE;
+    else if (!sg_inf && (sg_xz || !sg_grp)) c = BLST_POINT_NOT_IN_GROUP;
+    else if (kf & PKF_INF) c = BLST_PK_IS_INFINITY;
+    else if (kf & PKF_GRP) c = BLST_POINT_NOT_IN_GROUP;
+    else if (h_inf || sg_inf) c = BLST_VERIFY_FAIL;
+    else c = 0;
+    *code = c;
+  }
+}
+static_assert(VM_QCMIL_NIN == 21 && VM_QCPRE_W == 64 && VM_QCMIL_W == 64, "qcmil inputs: apk X Y Z, H, g");
+
 // FE(F_u) == 1 for unit u of the F planes (program final1): the shared body of the FE kernels.
 __device__ __forceinline__ bool fe_one(const VmDev& prog, const uint32_t* __restrict__ cst_g, Slab F, uint32_t u) {
   extern __shared__ uint4 lds4[];
@@ -1394,7 +1466,7 @@ struct ovh_ctx {
   // Fp-VM programs + constant table in device memory
   VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{},
       vm_pkchk{}, vm_g1padd{}, vm_sign0{}, vm_sign1{}, vm_vote1{}, vm_vote_t1{}, vm_final1{}, vm_votew{},
-      vm_votew_t{};
+      vm_votew_t{}, vm_qcpre{}, vm_qcmil{};
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
@@ -1438,6 +1510,8 @@ static constexpr uint32_t VOTE1_NSLOTS = VM_VOTE1_NSLOTS > VM_VOTE_T1_NSLOTS ? V
 static constexpr size_t LDS_VOTE1 = ((size_t)SLOT_BASE_W + VOTE1_NSLOTS * 12 + 4) * 4;
 static constexpr uint32_t VOTEW_NSLOTS = VM_VOTEW_NSLOTS > VM_VOTEW_T_NSLOTS ? VM_VOTEW_NSLOTS : VM_VOTEW_T_NSLOTS;
 static constexpr size_t LDS_VOTEW = ((size_t)SLOT_BASE_W + VOTEW_NSLOTS * 12 + 4) * 4;
+static constexpr size_t LDS_QCPRE = ((size_t)SLOT_BASE_W + VM_QCPRE_NSLOTS * 12 + 4) * 4;
+static constexpr size_t LDS_QCMIL = ((size_t)SLOT_BASE_W + VM_QCMIL_NSLOTS * 12) * 4;
 static constexpr size_t LDS_FINAL1 = ((size_t)SLOT_BASE_W + (size_t)VM_FINAL1_NSLOTS * 12) * 4;
 static constexpr size_t LDS_SIGN = ((size_t)SLOT_BASE_W + (64 / VM_SIGN0_W) * (size_t)SIGN_STRIDE_W) * 4;
 static constexpr size_t LDS_PKCHK = ((size_t)SLOT_BASE_W + (64 / VM_PKCHK_W) * (size_t)PKCHK_STRIDE_W) * 4;
@@ -1445,7 +1519,8 @@ static constexpr uint32_t G1PADD_STRIDE_W = align128w(VM_G1PADD_NSLOTS * 12);
 static constexpr size_t LDS_G1PADD = ((size_t)SLOT_BASE_W + (64 / VM_G1PADD_W) * (size_t)G1PADD_STRIDE_W) * 4;
 static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024 && LDS_SIGCHK <= 64 * 1024 &&
                   LDS_PKCHK <= 64 * 1024 && LDS_G1PADD <= 64 * 1024 && LDS_SIGN <= 64 * 1024 &&
-                  LDS_VOTE1 <= 64 * 1024 && LDS_FINAL1 <= 64 * 1024 && LDS_VOTEW <= 64 * 1024 && VM_G1PADD_NIN == 6,
+                  LDS_VOTE1 <= 64 * 1024 && LDS_FINAL1 <= 64 * 1024 && LDS_VOTEW <= 64 * 1024 && LDS_QCPRE <= 64 * 1024 &&
+                  LDS_QCMIL <= 64 * 1024 && VM_G1PADD_NIN == 6,
               "default LDS limit");
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
@@ -1506,6 +1581,10 @@ static int vm_init(ovh_ctx* c) {
                 VM_VOTE1_OUT, VM_VOTE1_NOUT));
   CHK(vm_upload(c, c->vm_vote_t1, VM_VOTE_T1_CODE, VM_VOTE_T1_NPHASES, VM_VOTE_T1_W, VM_VOTE_T1_NW, VM_VOTE_T1_IN,
                 VM_VOTE_T1_NIN, VM_VOTE_T1_OUT, VM_VOTE_T1_NOUT));
+  CHK(vm_upload(c, c->vm_qcpre, VM_QCPRE_CODE, VM_QCPRE_NPHASES, VM_QCPRE_W, VM_QCPRE_NW, VM_QCPRE_IN, VM_QCPRE_NIN,
+                VM_QCPRE_OUT, VM_QCPRE_NOUT));
+  CHK(vm_upload(c, c->vm_qcmil, VM_QCMIL_CODE, VM_QCMIL_NPHASES, VM_QCMIL_W, VM_QCMIL_NW, VM_QCMIL_IN, VM_QCMIL_NIN,
+                VM_QCMIL_OUT, VM_QCMIL_NOUT));
   CHK(vm_upload(c, c->vm_votew, VM_VOTEW_CODE, VM_VOTEW_NPHASES, VM_VOTEW_W, VM_VOTEW_NW, VM_VOTEW_IN, VM_VOTEW_NIN,
                 VM_VOTEW_OUT, VM_VOTEW_NOUT));
   CHK(vm_upload(c, c->vm_votew_t, VM_VOTEW_T_CODE, VM_VOTEW_T_NPHASES, VM_VOTEW_T_W, VM_VOTEW_T_NW, VM_VOTEW_T_IN,
@@ -3001,12 +3080,26 @@ static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_l
     c->qt_cap = cap;
   }
   CHK(ensure_qc_buf(c, 1));
+  CHK(ensure_cap(c, 2));
   CHK(ensure_in(c, n * 48 + 96 + 32 + 64));
-  uint8_t* d = c->in_buf;  // keys | sig | hash | code
+  uint8_t* d = c->in_buf;  // keys | sig | hash | code, qcpre flags
   int32_t* dc = (int32_t*)(d + ((n * 48 + 128 + 15) & ~(size_t)15));
+  uint32_t* qpf = (uint32_t*)(dc + 1);
   HIPCHK(hipMemcpyAsync(d, pks, n * 48, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(d + n * 48, agg_sig, 96, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipMemcpyAsync(d + n * 48 + 96, hash, 32, hipMemcpyHostToDevice, c->stream));
+  // the signature's checks, H(m) and Miller(-G1, sigma) on the side stream, beside the keys
+  int slot;
+  CHK(take_slot(c, &slot));
+  c->last_n = 0;
+  Slab s{c->state_slot[slot], c->cap};
+  HIPCHK(hipEventRecord(c->ev_x[2], c->stream));  // staged inputs
+  if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+  HIPCHK(hipStreamWaitEvent(c->xstream, c->ev_x[2], 0));
+  k_h2f<<<1, WG, 0, c->xstream>>>(1, d + n * 48 + 96, c->xmd, s);
+  k_vm_qcpre<<<1, 64, LDS_QCPRE, c->xstream>>>(c->vm_qcpre, c->vm_consts, d + n * 48, s, qpf);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(c->ev_x[3], c->xstream));
   uint32_t* kflags = c->qt_buf + (size_t)3 * 12 * c->qt_cap;
   constexpr uint32_t PK_SL = 64 / VM_PKCHK_W;
   k_vm_pkchk<<<(uint32_t)((n + PK_SL - 1) / PK_SL), 64, LDS_PKCHK, c->stream>>>((uint32_t)n, c->vm_pkchk, c->vm_consts, d,
@@ -3018,6 +3111,7 @@ static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_l
   uint32_t fl = 0;
   for (size_t i = 0; i < n; ++i) fl |= hf[i];
   // consensus.rs:454-458 order as sum_pks: any unparsable key -> "lose public key"
+  if (fl & (PKF_PARSE | PKF_GRP)) HIPCHK(hipStreamSynchronize(c->xstream));  // qcpre's buffers
   if (fl & PKF_PARSE) {
     *code = OVH_ERR_PUBKEY;
     return 0;
@@ -3038,9 +3132,14 @@ static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_l
     k_apk_finish<<<1, 64, 0, c->stream>>>(Slab{c->qt_buf + base, c->qt_cap}, Slab{c->qc_buf, c->qc_cap}, qflags);
   }
   HIPCHK(hipGetLastError());
-  CHK(ensure_cap(c, 1));
-  CHK(verify_one_locked(c, d + n * 48, d + n * 48 + 96, KeySrc{nullptr, PkSrc{c->qc_buf, c->qc_cap, qflags, nullptr}},
-                          dc));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_x[3], 0));
+  k_vm_qcmil<<<1, 64, LDS_QCMIL, c->stream>>>(c->vm_qcmil, c->vm_consts, PkSrc{c->qc_buf, c->qc_cap, qflags, nullptr}, s,
+                                              qpf, dc);
+  k_vm_final1<<<1, 64, LDS_FINAL1, c->stream>>>(c->vm_final1, c->vm_consts,
+                                                Slab{s.p + (size_t)S_F * 12 * s.cap + 1, s.cap}, dc,
+                                                c->result + RES_BATCH + slot);
+  HIPCHK(hipEventRecord(c->ev_back[slot], c->stream));
+  HIPCHK(hipGetLastError());
   CHK(sync_all(c));
   int32_t r = -1;
   HIPCHK(hipMemcpyAsync(&r, dc, 4, hipMemcpyDeviceToHost, c->stream));

@@ -242,3 +242,10 @@ def test_percall_programs_on_interpreter(hx, built, golden_votes, any_all):  # n
     o = run("votew", inp, r)
     assert run("final1", {"f%d" % j: o["st:f%d" % j] for j in range(12)}) == {"ok": 1}
     run("votew_t", tin, r)
+    # verify_aggregated_signature's split: qcpre (signature, H, Miller(-G1, sigma)) + qcmil
+    q = run("qcpre", {n: inp[n] for n in progs.QCPRE_IN})
+    mi = {"pk_X": tin["pk_X"], "pk_Y": tin["pk_Y"], "pk_Z": tin["pk_Z"]}
+    mi.update({"h%d" % k: q["st:h%d" % k] for k in range(6)})
+    mi.update({"g%d" % k: q["st:g%d" % k] for k in range(12)})
+    o = run("qcmil", mi)
+    assert run("final1", {"f%d" % j: o["st:f%d" % j] for j in range(12)}) == {"ok": 1}

@@ -219,6 +219,50 @@ def build_votew(table: bool):
     return build
 
 
+QCPRE_IN = ["sig_x0", "sig_x1", "sig_sort", "u00", "u01", "u10", "u11"]
+QCPRE_OUT = ["sig_ok", "sig_grp", "h_inf"]
+QCPRE_ST = [(n, S_RS + k) for k, n in enumerate(g2p_names("h"))] + [(n, S_F + k) for k, n in enumerate(f12_names("g"))]
+QCMIL_IN = ["pk_X", "pk_Y", "pk_Z"] + g2p_names("h") + f12_names("g")
+
+
+def build_qcpre():
+    """verify_aggregated_signature, the part that does not need the aggregated key (it runs on a
+    side stream beside the keys' decompression, subgroup checks and tree sum): the signature's
+    decompression + G2 subgroup check, H = hash_to_G2(u0, u1) and g = Miller(-G1, sigma); H
+    (projective) and g go to HBM planes for qcmil."""
+    p = Prog("qcpre")
+    a = Alg(p, use_sop=USE_SOP, fast_sqrt=True)
+    R = p.const(R_MONT)
+    sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
+    u0 = (p.input("u00"), p.input("u01"))
+    u1 = (p.input("u10"), p.input("u11"))
+    sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
+    Qs = (qx, qy, (p.one, p.zero))
+    sig_grp = a.g2_in_group(Qs)
+    H = a.hash_to_g2(u0, u1)
+    h_inf = a.f2_is_zero(H[2])
+    g = a.miller_loop_multi([((p.const(G1X), p.const(-G1Y)), Qs)])
+    for name, v in zip(QCPRE_OUT, [sig_ok, sig_grp, h_inf]):
+        p.output(name, v)
+    for (name, plane), v in zip(QCPRE_ST, flat_g2p(H) + flat12(g)):
+        p.store(name, v, plane)
+    return p
+
+
+def build_qcmil():
+    """verify_aggregated_signature, the rest: f = Miller(apk, H) * g (apk projective, from the
+    key tree), then final1."""
+    p = Prog("qcmil")
+    a = Alg(p, use_sop=USE_SOP)
+    P = (p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z"))
+    H = unflat_g2p([p.input(n) for n in g2p_names("h")])
+    g = unflat12([p.input(n) for n in f12_names("g")])
+    f = a.f12_mul(a.miller_loop_multi([(P, H)]), g)
+    for (name, plane), v in zip(VOTE1_ST, flat12(f)):
+        p.store(name, v, plane)
+    return p
+
+
 def build_final1():
     p = Prog("final1")
     a = Alg(p, inv_op=True, use_sop=USE_SOP)
@@ -453,6 +497,8 @@ PROGRAMS["pkchk"] = (build_pkchk, PKCHK_IN, PKCHK_OUT)
 PROGRAMS["vote1"] = (build_vote1(False), VOTE_IN, VOTE_OUT)
 PROGRAMS["vote_t1"] = (build_vote1(True), VOTE_T_IN, VOTE_T_OUT)
 PROGRAMS["final1"] = (build_final1, f12_names("f"), ["ok"])
+PROGRAMS["qcpre"] = (build_qcpre, QCPRE_IN, QCPRE_OUT)
+PROGRAMS["qcmil"] = (build_qcmil, QCMIL_IN, [])
 PROGRAMS["votew"] = (build_votew(False), VOTE_IN, VOTE_OUT)
 PROGRAMS["votew_t"] = (build_votew(True), VOTE_T_IN, VOTE_T_OUT)
 PROGRAMS["sign0"] = (build_sign0, SIGN0_IN, SIGN_ACC + SIGN_H)
