@@ -36,6 +36,7 @@ SIGNATURES = [
     ("ovh_prefetch", ctypes.c_int, [_vp, _sz, _u8p, _u8p, _u8p]),
     ("ovh_cache_config", ctypes.c_int, [_vp, _sz]),
     ("ovh_cache_stats", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
+    ("ovh_msg_cache_stats", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
     ("ovh_verify_qc_batch", ctypes.c_int, [_vp, _sz, _u8p, _u8p, _u8p, _sz, _vp]),
     ("ovh_set_test_rlc", ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64]),
     ("ovh_verify_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp]),

@@ -532,12 +532,20 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
 static_assert(VM_VOTEW_NIN == VM_VOTE1_NIN && VM_VOTEW_T_NIN == VM_VOTE_T1_NIN && VM_VOTEW_W == 64 &&
                   VM_VOTEW_T_W == 64 && VM_VOTE1_W == 64 && VM_VOTE_T1_W == 64,
               "one-vote-per-wave programs share the vote1 / vote_t1 layouts");
-template <bool TABLE>
+// HIN (vote1h / vote_t1h): H = hash_to_G2(hash) comes from the message cache (planes hc, entry
+// he, flag *hinf_in) instead of the u planes; otherwise *hinf_out (if set) receives the
+// program's H-is-infinity flag for the cache.
+static_assert(VM_VOTE1H_IN_H0 == VM_VOTE1_IN_U00 && VM_VOTE_T1H_IN_H0 == VM_VOTE_T1_IN_U00 &&
+                  VM_VOTE1H_OUT_SIG_GRP == VM_VOTE1_OUT_SIG_GRP && VM_VOTE_T1H_OUT_SIG_GRP == VM_VOTE_T1_OUT_SIG_GRP,
+              "vote1h / vote_t1h share vote1 / vote_t1's layouts, H in place of the u's");
+template <bool TABLE, bool HIN = false>
 __device__ __forceinline__ void vote_wave(const VmDev& prog, uint32_t nph, uint32_t ns, const uint16_t* IN,
                                           const uint16_t* OUT, const uint32_t* __restrict__ cst_g,
                                           const uint8_t* __restrict__ pk_bytes, PkSrc pk, uint32_t e,
                                           const uint8_t* __restrict__ sig, Slab s, uint32_t i, uint64_t scalar,
-                                          int32_t* __restrict__ code) {
+                                          int32_t* __restrict__ code, Slab hc = Slab{nullptr, 0}, uint32_t he = 0,
+                                          const uint32_t* __restrict__ hinf_in = nullptr,
+                                          uint32_t* __restrict__ hinf_out = nullptr) {
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -568,11 +576,16 @@ __device__ __forceinline__ void vote_wave(const VmDev& prog, uint32_t nph, uint3
       slot_flag(slots, IN[VM_VOTE1_IN_PK_SORT], sort);
       hdr[1] = bad | inf << 1 | xz << 2;
     }
-  } else if (lane >= 2 && lane < 6) {
+  } else if (!HIN && lane >= 2 && lane < 6) {
     Fp u;
     s.ld(u, S_U + (lane - 2), i);
     if constexpr (TABLE) slot_put(slots, IN[VM_VOTE_T1_IN_U00 + (lane - 2)], u.v);
     else slot_put(slots, IN[VM_VOTE1_IN_U00 + (lane - 2)], u.v);
+  } else if (HIN && lane >= 10 && lane < 16) {
+    Fp h;
+    hc.ld(h, lane - 10, he);
+    if constexpr (TABLE) slot_put(slots, IN[VM_VOTE_T1_IN_U00 + (lane - 10)], h.v);
+    else slot_put(slots, IN[VM_VOTE1_IN_U00 + (lane - 10)], h.v);
   } else if (TABLE && lane >= 6 && lane < 9) {
     Fp v;
     Slab{const_cast<uint32_t*>(pk.planes), pk.cap}.ld(v, lane - 6, e);
@@ -587,14 +600,15 @@ __device__ __forceinline__ void vote_wave(const VmDev& prog, uint32_t nph, uint3
     if constexpr (TABLE) {
       sg_ok = slot_flag_get(slots, OUT[VM_VOTE_T1_OUT_SIG_OK]);
       sg_grp = slot_flag_get(slots, OUT[VM_VOTE_T1_OUT_SIG_GRP]);
-      h_inf = slot_flag_get(slots, OUT[VM_VOTE_T1_OUT_H_INF]);
+      h_inf = HIN ? *hinf_in : slot_flag_get(slots, OUT[VM_VOTE_T1_OUT_H_INF]);
     } else {
       pk_ok = slot_flag_get(slots, OUT[VM_VOTE1_OUT_PK_OK]);
       pk_grp = slot_flag_get(slots, OUT[VM_VOTE1_OUT_PK_GRP]);
       sg_ok = slot_flag_get(slots, OUT[VM_VOTE1_OUT_SIG_OK]);
       sg_grp = slot_flag_get(slots, OUT[VM_VOTE1_OUT_SIG_GRP]);
-      h_inf = slot_flag_get(slots, OUT[VM_VOTE1_OUT_H_INF]);
+      h_inf = HIN ? *hinf_in : slot_flag_get(slots, OUT[VM_VOTE1_OUT_H_INF]);
     }
+    if (!HIN && hinf_out) *hinf_out = h_inf;
     // key flags in the table's terms, then the precedence of k_vm_vote_t (consensus.rs:397-416)
     uint32_t kf = pf;
     if (!TABLE) {
@@ -619,14 +633,35 @@ __device__ __forceinline__ void vote_wave(const VmDev& prog, uint32_t nph, uint3
 template <bool TABLE>
 __global__ __launch_bounds__(64) void k_vm_vote1(VmDev prog, const uint32_t* __restrict__ cst_g,
                                                  const uint8_t* __restrict__ pk_bytes, PkSrc pk,
-                                                 const uint8_t* __restrict__ sig, Slab s, int32_t* __restrict__ code) {
+                                                 const uint8_t* __restrict__ sig, Slab s, int32_t* __restrict__ code,
+                                                 uint32_t* __restrict__ hinf_out = nullptr) {
   const uint32_t e = TABLE && pk.idx ? (uint32_t)pk.idx[0] : 0u;
   if constexpr (TABLE)
     vote_wave<true>(prog, VM_VOTE_T1_NPHASES, VM_VOTE_T1_NSLOTS, VM_VOTE_T1_IN, VM_VOTE_T1_OUT, cst_g, pk_bytes, pk, e,
-                    sig, s, 0, 1, code);
+                    sig, s, 0, 1, code, Slab{nullptr, 0}, 0, nullptr, hinf_out);
   else
     vote_wave<false>(prog, VM_VOTE1_NPHASES, VM_VOTE1_NSLOTS, VM_VOTE1_IN, VM_VOTE1_OUT, cst_g, pk_bytes, pk, e, sig,
-                     s, 0, 1, code);
+                     s, 0, 1, code, Slab{nullptr, 0}, 0, nullptr, hinf_out);
+}
+
+// The standalone vote on a hash in the message cache: vote1h / vote_t1h with H from entry he.
+template <bool TABLE>
+__global__ __launch_bounds__(64) void k_vm_vote1h(VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                  const uint8_t* __restrict__ pk_bytes, PkSrc pk,
+                                                  const uint8_t* __restrict__ sig, Slab s, int32_t* __restrict__ code,
+                                                  Slab hc, uint32_t he, const uint32_t* __restrict__ hinf) {
+  const uint32_t e = TABLE && pk.idx ? (uint32_t)pk.idx[0] : 0u;
+  if constexpr (TABLE)
+    vote_wave<true, true>(prog, VM_VOTE_T1H_NPHASES, VM_VOTE_T1H_NSLOTS, VM_VOTE_T1H_IN, VM_VOTE_T1H_OUT, cst_g,
+                          pk_bytes, pk, e, sig, s, 0, 1, code, hc, he, hinf + he);
+  else
+    vote_wave<false, true>(prog, VM_VOTE1H_NPHASES, VM_VOTE1H_NSLOTS, VM_VOTE1H_IN, VM_VOTE1H_OUT, cst_g, pk_bytes, pk,
+                           e, sig, s, 0, 1, code, hc, he, hinf + he);
+}
+
+// vote1's stored H (the S_RS planes of slab index 0) -> message-cache entry he.
+__global__ __launch_bounds__(64) void k_copy_h(Slab s, Slab hc, uint32_t he) {
+  for (uint32_t k = threadIdx.x; k < 6 * 12; k += 64) hc.p[(size_t)k * hc.cap + he] = s.p[(size_t)(S_RS * 12 + k) * s.cap];
 }
 
 // Small batches (n <= SMALL_MAX, verify_small_locked): vote i = workgroup i on a whole wave,
@@ -1466,7 +1501,15 @@ struct ovh_ctx {
   // Fp-VM programs + constant table in device memory
   VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{},
       vm_pkchk{}, vm_g1padd{}, vm_sign0{}, vm_sign1{}, vm_vote1{}, vm_vote_t1{}, vm_final1{}, vm_votew{},
-      vm_votew_t{}, vm_qcpre{}, vm_qcmil{};
+      vm_votew_t{}, vm_qcpre{}, vm_qcmil{}, vm_vote1h{}, vm_vote_t1h{};
+  // message cache (verify_one_locked): H = hash_to_G2(hash) of the last HC_CAP hashes verified
+  // per call, projective planes + H-is-infinity flags, FIFO replacement
+  uint32_t* hc_planes = nullptr;
+  uint32_t* hc_inf = nullptr;
+  std::unordered_map<std::string, uint32_t> hc_index;
+  std::vector<std::string> hc_keys;
+  uint32_t hc_next = 0;
+  uint64_t hc_hits = 0, hc_misses = 0;
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
@@ -1508,6 +1551,8 @@ static_assert(VM_MADD_W == VM_PADD_W && VM_HDBL1_W == VM_HDBL2_W && VM_HDBL1_W =
 static constexpr size_t LDS_SIGCHK = ((size_t)SLOT_BASE_W + (64 / VM_SIGCHK_W) * (size_t)SIGCHK_STRIDE_W) * 4;
 static constexpr uint32_t VOTE1_NSLOTS = VM_VOTE1_NSLOTS > VM_VOTE_T1_NSLOTS ? VM_VOTE1_NSLOTS : VM_VOTE_T1_NSLOTS;
 static constexpr size_t LDS_VOTE1 = ((size_t)SLOT_BASE_W + VOTE1_NSLOTS * 12 + 4) * 4;
+static constexpr uint32_t VOTE1H_NSLOTS = VM_VOTE1H_NSLOTS > VM_VOTE_T1H_NSLOTS ? VM_VOTE1H_NSLOTS : VM_VOTE_T1H_NSLOTS;
+static constexpr size_t LDS_VOTE1H = ((size_t)SLOT_BASE_W + VOTE1H_NSLOTS * 12 + 4) * 4;
 static constexpr uint32_t VOTEW_NSLOTS = VM_VOTEW_NSLOTS > VM_VOTEW_T_NSLOTS ? VM_VOTEW_NSLOTS : VM_VOTEW_T_NSLOTS;
 static constexpr size_t LDS_VOTEW = ((size_t)SLOT_BASE_W + VOTEW_NSLOTS * 12 + 4) * 4;
 static constexpr size_t LDS_QCPRE = ((size_t)SLOT_BASE_W + VM_QCPRE_NSLOTS * 12 + 4) * 4;
@@ -1519,7 +1564,7 @@ static constexpr uint32_t G1PADD_STRIDE_W = align128w(VM_G1PADD_NSLOTS * 12);
 static constexpr size_t LDS_G1PADD = ((size_t)SLOT_BASE_W + (64 / VM_G1PADD_W) * (size_t)G1PADD_STRIDE_W) * 4;
 static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024 && LDS_SIGCHK <= 64 * 1024 &&
                   LDS_PKCHK <= 64 * 1024 && LDS_G1PADD <= 64 * 1024 && LDS_SIGN <= 64 * 1024 &&
-                  LDS_VOTE1 <= 64 * 1024 && LDS_FINAL1 <= 64 * 1024 && LDS_VOTEW <= 64 * 1024 && LDS_QCPRE <= 64 * 1024 &&
+                  LDS_VOTE1 <= 64 * 1024 && LDS_FINAL1 <= 64 * 1024 && LDS_VOTEW <= 64 * 1024 && LDS_QCPRE <= 64 * 1024 && LDS_VOTE1H <= 64 * 1024 &&
                   LDS_QCMIL <= 64 * 1024 && VM_G1PADD_NIN == 6,
               "default LDS limit");
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
@@ -1581,6 +1626,10 @@ static int vm_init(ovh_ctx* c) {
                 VM_VOTE1_OUT, VM_VOTE1_NOUT));
   CHK(vm_upload(c, c->vm_vote_t1, VM_VOTE_T1_CODE, VM_VOTE_T1_NPHASES, VM_VOTE_T1_W, VM_VOTE_T1_NW, VM_VOTE_T1_IN,
                 VM_VOTE_T1_NIN, VM_VOTE_T1_OUT, VM_VOTE_T1_NOUT));
+  CHK(vm_upload(c, c->vm_vote1h, VM_VOTE1H_CODE, VM_VOTE1H_NPHASES, VM_VOTE1H_W, VM_VOTE1H_NW, VM_VOTE1H_IN,
+                VM_VOTE1H_NIN, VM_VOTE1H_OUT, VM_VOTE1H_NOUT));
+  CHK(vm_upload(c, c->vm_vote_t1h, VM_VOTE_T1H_CODE, VM_VOTE_T1H_NPHASES, VM_VOTE_T1H_W, VM_VOTE_T1H_NW, VM_VOTE_T1H_IN,
+                VM_VOTE_T1H_NIN, VM_VOTE_T1H_OUT, VM_VOTE_T1H_NOUT));
   CHK(vm_upload(c, c->vm_qcpre, VM_QCPRE_CODE, VM_QCPRE_NPHASES, VM_QCPRE_W, VM_QCPRE_NW, VM_QCPRE_IN, VM_QCPRE_NIN,
                 VM_QCPRE_OUT, VM_QCPRE_NOUT));
   CHK(vm_upload(c, c->vm_qcmil, VM_QCMIL_CODE, VM_QCMIL_NPHASES, VM_QCMIL_W, VM_QCMIL_NW, VM_QCMIL_IN, VM_QCMIL_NIN,
@@ -1969,18 +2018,62 @@ static int side_front(ovh_ctx* c, int slot, uint32_t n, bool pipe, uint32_t unti
 // batch's vote workgroups are resident.
 // One standalone vote on the main stream (k_h2f, k_vm_vote1 / k_vm_vote_t1, k_vm_final1): its
 // own pairing equation, no coefficient (section 1 of DESIGN.md). Caller holds c->mu and waits.
-static int verify_one_locked(ovh_ctx* c, const uint8_t* d_sig, const uint8_t* d_hash, KeySrc key, int32_t* d_code) {
+// h_host: the hash's host bytes, for the message cache (every vote of a round signs the same
+// hash): a hash seen before runs vote1h / vote_t1h on its cached H, without hash_to_G2 (vote1
+// 2,061 -> 1,444 phases); a new one runs vote1 / vote_t1, whose stored H is copied into the
+// cache (FIFO, HC_CAP entries). Null: no cache.
+#define HC_CAP 256u
+static int verify_one_locked(ovh_ctx* c, const uint8_t* d_sig, const uint8_t* d_hash, KeySrc key, int32_t* d_code,
+                             const uint8_t* h_host = nullptr) {
   CHK(ensure_cap(c, 1));
   int slot;
   CHK(take_slot(c, &slot));
   c->last_n = 0;  // no partial state for ovh_batch_partial_device / fallback
   Slab s{c->state_slot[slot], c->cap};
   hipStream_t st = c->stream;
+  if (h_host && !c->hc_planes) {
+    HIPCHK(hipMalloc(&c->hc_planes, (size_t)6 * 12 * HC_CAP * 4));
+    HIPCHK(hipMalloc(&c->hc_inf, (size_t)HC_CAP * 4));
+    c->hc_keys.assign(HC_CAP, std::string());
+  }
+  const Slab hc{c->hc_planes, HC_CAP};
+  std::string hk;
+  if (h_host) {
+    hk.assign((const char*)h_host, 32);
+    auto it = c->hc_index.find(hk);
+    if (it != c->hc_index.end()) {
+      ++c->hc_hits;
+      const uint32_t he = it->second;
+      if (key.bytes)
+        k_vm_vote1h<false><<<1, 64, LDS_VOTE1H, st>>>(c->vm_vote1h, c->vm_consts, key.bytes, PkSrc{}, d_sig, s, d_code,
+                                                      hc, he, c->hc_inf);
+      else
+        k_vm_vote1h<true><<<1, 64, LDS_VOTE1H, st>>>(c->vm_vote_t1h, c->vm_consts, nullptr, key.pts, d_sig, s, d_code,
+                                                     hc, he, c->hc_inf);
+      k_vm_final1<<<1, 64, LDS_FINAL1, st>>>(c->vm_final1, c->vm_consts, Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap},
+                                              d_code, c->result + RES_BATCH + slot);
+      HIPCHK(hipEventRecord(c->ev_back[slot], st));
+      HIPCHK(hipGetLastError());
+      return 0;
+    }
+    ++c->hc_misses;
+  }
+  uint32_t he = 0;
+  if (h_host) {  // the entry is filled in stream order, before any later call can read it
+    he = c->hc_next;
+    c->hc_next = (c->hc_next + 1) % HC_CAP;
+    if (!c->hc_keys[he].empty()) c->hc_index.erase(c->hc_keys[he]);
+    c->hc_keys[he] = hk;
+    c->hc_index[hk] = he;
+  }
   k_h2f<<<1, WG, 0, st>>>(1, d_hash, c->xmd, s);
   if (key.bytes)
-    k_vm_vote1<false><<<1, 64, LDS_VOTE1, st>>>(c->vm_vote1, c->vm_consts, key.bytes, PkSrc{}, d_sig, s, d_code);
+    k_vm_vote1<false><<<1, 64, LDS_VOTE1, st>>>(c->vm_vote1, c->vm_consts, key.bytes, PkSrc{}, d_sig, s, d_code,
+                                                h_host ? c->hc_inf + he : nullptr);
   else
-    k_vm_vote1<true><<<1, 64, LDS_VOTE1, st>>>(c->vm_vote_t1, c->vm_consts, nullptr, key.pts, d_sig, s, d_code);
+    k_vm_vote1<true><<<1, 64, LDS_VOTE1, st>>>(c->vm_vote_t1, c->vm_consts, nullptr, key.pts, d_sig, s, d_code,
+                                               h_host ? c->hc_inf + he : nullptr);
+  if (h_host) k_copy_h<<<1, 64, 0, st>>>(s, hc, he);
   k_vm_final1<<<1, 64, LDS_FINAL1, st>>>(c->vm_final1, c->vm_consts, Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap},
                                           d_code, c->result + RES_BATCH + slot);
   HIPCHK(hipEventRecord(c->ev_back[slot], st));
@@ -2166,7 +2259,7 @@ static int verify_host_locked(ovh_ctx* c, size_t n, const uint8_t* sigs, const u
   CHK(stage_split(c, n, sigs, hashes, pks, &d, &t, perm));
   int32_t* dc = (int32_t*)(d + n * 176);
   if (n == 1) {
-    CHK(verify_one_locked(c, d, d + 96, staged_key(c, n, d, t, 0), dc));
+    CHK(verify_one_locked(c, d, d + 96, staged_key(c, n, d, t, 0), dc, hashes));
   } else {
     for (int part = 0; part < 2; ++part) {  // table votes [0, t), then the others [t, n)
       const size_t lo = part ? t : 0, cnt = part ? n - t : t;
@@ -2674,7 +2767,7 @@ static void destroy_one(ovh_ctx* c) {
       if (p) (void)hipFree(p);
   for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vstart, (void*)c->vm_consts,
                   (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
-                  (void*)c->tab.planes, (void*)c->tab.flags, (void*)c->qc_buf, (void*)c->qt_buf, (void*)c->gather,
+                  (void*)c->tab.planes, (void*)c->tab.flags, (void*)c->qc_buf, (void*)c->qt_buf, (void*)c->hc_planes, (void*)c->hc_inf, (void*)c->gather,
                   (void*)c->mfin})
     if (p) (void)hipFree(p);
   for (void* p : c->vm_bufs) (void)hipFree(p);
@@ -2877,7 +2970,7 @@ int ovh_verify(ovh_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* ha
     std::vector<uint32_t> perm;
     CHK(stage_split(s, 1, sig, hash, pk, &d, &t, perm));
     int32_t* dc = (int32_t*)(d + 176);
-    CHK(verify_one_locked(s, d, d + 96, staged_key(s, 1, d, t, 0), dc));
+    CHK(verify_one_locked(s, d, d + 96, staged_key(s, 1, d, t, 0), dc, hash));
     int32_t out = -1;
     HIPCHK(hipMemcpyAsync(&out, dc, 4, hipMemcpyDeviceToHost, s->stream));
     HIPCHK(hipStreamSynchronize(s->stream));
@@ -3279,6 +3372,17 @@ int ovh_cache_stats(ovh_ctx* c, uint64_t stats[3]) {
   stats[0] = c->cache.hits;
   stats[1] = c->cache.misses;
   stats[2] = c->cache.map.size();
+  return 0;
+}
+
+int ovh_msg_cache_stats(ovh_ctx* c, uint64_t stats[2]) {
+  if (!c || !stats) return OVH_ERR_ARG;
+  stats[0] = stats[1] = 0;
+  for (ovh_ctx* s : devices_of(c)) {
+    std::lock_guard<std::mutex> g(s->mu);
+    stats[0] += s->hc_hits;
+    stats[1] += s->hc_misses;
+  }
   return 0;
 }
 

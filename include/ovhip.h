@@ -141,6 +141,11 @@ int ovh_prefetch(ovh_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* has
 int ovh_cache_config(ovh_ctx* ctx, size_t capacity);
 /* stats[0] = hits, stats[1] = misses (fixed-size triples not in the cache), stats[2] = entries. */
 int ovh_cache_stats(ovh_ctx* ctx, uint64_t stats[3]);
+/* Message cache of the per-call verify (ovh_verify, ovh_verify_batch with n = 1): H =
+ * hash_to_G2(hash) of the last 256 hashes verified per call, so every later vote on a hash (all
+ * votes of a round sign the same hash, consensus.rs:397-416) skips hash_to_G2. stats[0] = hits,
+ * stats[1] = misses, summed over a multi-device context's devices. */
+int ovh_msg_cache_stats(ovh_ctx* ctx, uint64_t stats[2]);
 
 /* Batched QC verification for block sync (check_block, consensus.rs:143-207): QC j = aggregated
  * signature sigs[j] (96 B) over hashes[j] (32 B, the SM3 of rlp(Vote{h, r, Precommit, block})),

@@ -175,6 +175,47 @@ def build_vote1(table: bool):
             p.output(name, v)
         for (name, plane), v in zip(VOTE1_ST, flat12(f)):
             p.store(name, v, plane)
+        # H (projective) for the message cache (ovhip.hip verify_one_locked): the next vote on
+        # the same hash runs vote1h without hash_to_G2
+        for (name, plane), v in zip(VOTE1H_ST, flat_g2p(H)):
+            p.store(name, v, plane)
+        return p
+    return build
+
+
+VOTE1H_ST = [(n, S_RS + k) for k, n in enumerate(g2p_names("h"))]
+VOTE1H_IN = ["pk_x", "pk_sort", "sig_x0", "sig_x1", "sig_sort"] + g2p_names("h")
+VOTE1H_OUT = ["pk_ok", "pk_grp", "sig_ok", "sig_grp"]
+VOTE_T1H_IN = ["pk_X", "pk_Y", "pk_Z", "sig_x0", "sig_x1", "sig_sort"] + g2p_names("h")
+VOTE_T1H_OUT = ["sig_ok", "sig_grp"]
+
+
+def build_vote1h(table: bool):
+    """vote1h / vote_t1h: vote1 / vote_t1 with H = hash_to_G2(hash) from the message cache (a
+    vote on a hash already seen by this context: every vote of a round signs the same hash).
+    Critical path: the key's decompression and Miller loop, beside the signature's (1,250 levels
+    instead of hash_to_G2's 1,203 plus the Miller loop)."""
+    def build():
+        p = Prog("vote_t1h" if table else "vote1h")
+        a = Alg(p, use_sop=USE_SOP, fast_sqrt=True)
+        R = p.const(R_MONT)
+        if table:
+            Pa = (p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z"))
+        else:
+            pk_ok, (px, py) = a.g1_decompress(p.input("pk_x") * R, p.input("pk_sort"))
+            pk_grp, _ = a.g1_in_group((px, py, p.one))
+            Pa = (px, py)
+        sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
+        H = unflat_g2p([p.input(n) for n in g2p_names("h")])
+        sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
+        Qs = (qx, qy, (p.one, p.zero))
+        sig_grp = a.g2_in_group(Qs)
+        f = a.f12_mul(a.miller_loop_multi([(Pa, H)]), a.miller_loop_multi([((p.const(G1X), p.const(-G1Y)), Qs)]))
+        flags = [sig_ok, sig_grp] if table else [pk_ok, pk_grp, sig_ok, sig_grp]
+        for name, v in zip(VOTE_T1H_OUT if table else VOTE1H_OUT, flags):
+            p.output(name, v)
+        for (name, plane), v in zip(VOTE1_ST, flat12(f)):
+            p.store(name, v, plane)
         return p
     return build
 
@@ -497,6 +538,8 @@ PROGRAMS["pkchk"] = (build_pkchk, PKCHK_IN, PKCHK_OUT)
 PROGRAMS["vote1"] = (build_vote1(False), VOTE_IN, VOTE_OUT)
 PROGRAMS["vote_t1"] = (build_vote1(True), VOTE_T_IN, VOTE_T_OUT)
 PROGRAMS["final1"] = (build_final1, f12_names("f"), ["ok"])
+PROGRAMS["vote1h"] = (build_vote1h(False), VOTE1H_IN, VOTE1H_OUT)
+PROGRAMS["vote_t1h"] = (build_vote1h(True), VOTE_T1H_IN, VOTE_T1H_OUT)
 PROGRAMS["qcpre"] = (build_qcpre, QCPRE_IN, QCPRE_OUT)
 PROGRAMS["qcmil"] = (build_qcmil, QCMIL_IN, [])
 PROGRAMS["votew"] = (build_votew(False), VOTE_IN, VOTE_OUT)
