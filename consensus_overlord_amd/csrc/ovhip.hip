@@ -999,6 +999,63 @@ __global__ __launch_bounds__(64) void k_g2p_compress(Slab in, uint8_t* out) {
 // scalar (2-bit windows), sign1 runs three times for the rest: the scalar enters only as the
 // selb bits of each launch, so the instruction stream does not depend on it. Lane 0 of the
 // slice compresses the result.
+// Public keys from secret scalars (ovh_sk_to_pk, ovh_sk_to_pk_batch_device): program pkgen four
+// times from the identity, acc -> [2^64] acc + [k] G1 over the scalar's 64-bit chunks (most
+// significant first; the secret enters only as selb bits), on a 16-lane slice per key, then one
+// lane converts (X : Y : Z) to Jacobian coordinates and compresses (one inversion).
+constexpr uint32_t PKGEN_STRIDE_W = align256w(VM_PKGEN_NSLOTS * 12 + 3 * 12);
+__global__ __launch_bounds__(64) void k_vm_pkgen(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                 const uint8_t* __restrict__ sks, uint8_t* __restrict__ out) {
+  static_assert(VM_PKGEN_NIN == 3 && VM_PKGEN_NOUT == 3, "pkgen program shape (tools/fpvm/progs.py)");
+  constexpr uint32_t W = VM_PKGEN_W;
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / W, lane = threadIdx.x % W;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * PKGEN_STRIDE_W;
+  uint32_t* acc = slots + VM_PKGEN_NSLOTS * 12;  // (X, Y, Z) between the launches
+  const uint32_t i = blockIdx.x * (64 / W) + slice;
+  const bool active = i < n;
+  load_consts(cst, cst_g, VM_NCONST);
+  uint64_t k[4] = {0, 0, 0, 0};  // big-endian 64-bit chunks, k[0] the most significant
+  if (active) {
+    const uint8_t* b = sks + (size_t)i * 32;
+    for (int j = 0; j < 4; ++j)
+      for (int t = 0; t < 8; ++t) k[j] = k[j] << 8 | b[8 * j + t];
+    if (lane < 3)
+      for (int l = 0; l < 12; ++l) acc[lane * 12 + l] = lane == 1 ? ONE_M[l] : 0u;  // the identity (0 : 1 : 0)
+  }
+  __syncthreads();
+  for (int r = 0; r < 4; ++r) {
+    if (active && lane < 3) slot_put(slots, VM_PKGEN_IN[lane], acc + lane * 12);
+    __syncthreads();
+    vm::run(prog.code, VM_PKGEN_NPHASES, W, lane, active, slots, cst, k[r], vm::Out{nullptr, 0, 0});
+    __syncthreads();
+    if (active && lane < 3) {
+      Fp t;
+      for (int l = 0; l < 12; ++l) t.v[l] = slots[VM_PKGEN_OUT[lane] * 12 + l];
+      vm::canon(t, t);
+      for (int l = 0; l < 12; ++l) acc[lane * 12 + l] = t.v[l];
+    }
+    __syncthreads();
+  }
+  k[0] = k[1] = k[2] = k[3] = 0;
+  if (active && lane == 0) {
+    Fp X, Y, Z, zz;
+    for (int l = 0; l < 12; ++l) {
+      X.v[l] = acc[l];
+      Y.v[l] = acc[12 + l];
+      Z.v[l] = acc[24 + l];
+    }
+    G1J j;  // (X : Y : Z) homogeneous = (X Z : Y Z^2 : Z) Jacobian
+    fp_mul(j.X, X, Z);
+    fp_sqr(zz, Z);
+    fp_mul(j.Y, Y, zz);
+    j.Z = Z;
+    g1_compress(out + (size_t)i * 48, j);
+  }
+}
+
 constexpr uint32_t SIGN_NSLOTS = VM_SIGN0_NSLOTS > VM_SIGN1_NSLOTS ? VM_SIGN0_NSLOTS : VM_SIGN1_NSLOTS;
 constexpr uint32_t SIGN_STRIDE_W = align256w(SIGN_NSLOTS * 12 + 24 * 12);  // + acc, H, 2H, 3H stash
 __global__ __launch_bounds__(64) void k_vm_sign(uint32_t n, VmDev p0, VmDev p1, const uint32_t* __restrict__ cst_g,
@@ -1379,19 +1436,6 @@ __device__ void sk_words(uint32_t k[8], const uint8_t* sk) {
   }
 }
 
-__global__ __launch_bounds__(WG) void k_sk_to_pk(uint32_t n, const uint8_t* __restrict__ sks, uint8_t* __restrict__ pks) {
-  const uint32_t i = blockIdx.x * WG + threadIdx.x;
-  if (i >= n) return;
-  uint32_t k[8];
-  sk_words(k, sks + (size_t)i * 32);
-  G1J g, p;
-  fp_load(g.X, G1X_M);
-  fp_load(g.Y, G1Y_M);
-  fp_one(g.Z);
-  jac_mul_words(p, g, k, 8);
-  g1_compress(pks + (size_t)i * 48, p);
-}
-
 // ------------------------------------------------------------------------ host side
 // Validator table (ovh_set_validators): keys as points in HBM + host lookup structures.
 struct ValidatorTable {
@@ -1501,7 +1545,7 @@ struct ovh_ctx {
   // Fp-VM programs + constant table in device memory
   VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{},
       vm_pkchk{}, vm_g1padd{}, vm_sign0{}, vm_sign1{}, vm_vote1{}, vm_vote_t1{}, vm_final1{}, vm_votew{},
-      vm_votew_t{}, vm_qcpre{}, vm_qcmil{}, vm_vote1h{}, vm_vote_t1h{};
+      vm_votew_t{}, vm_qcpre{}, vm_qcmil{}, vm_vote1h{}, vm_vote_t1h{}, vm_pkgen{};
   // message cache (verify_one_locked): H = hash_to_G2(hash) of the last HC_CAP hashes verified
   // per call, projective planes + H-is-infinity flags, FIFO replacement
   uint32_t* hc_planes = nullptr;
@@ -1559,11 +1603,12 @@ static constexpr size_t LDS_QCPRE = ((size_t)SLOT_BASE_W + VM_QCPRE_NSLOTS * 12 
 static constexpr size_t LDS_QCMIL = ((size_t)SLOT_BASE_W + VM_QCMIL_NSLOTS * 12) * 4;
 static constexpr size_t LDS_FINAL1 = ((size_t)SLOT_BASE_W + (size_t)VM_FINAL1_NSLOTS * 12) * 4;
 static constexpr size_t LDS_SIGN = ((size_t)SLOT_BASE_W + (64 / VM_SIGN0_W) * (size_t)SIGN_STRIDE_W) * 4;
+static constexpr size_t LDS_PKGEN = ((size_t)SLOT_BASE_W + (64 / VM_PKGEN_W) * (size_t)PKGEN_STRIDE_W) * 4;
 static constexpr size_t LDS_PKCHK = ((size_t)SLOT_BASE_W + (64 / VM_PKCHK_W) * (size_t)PKCHK_STRIDE_W) * 4;
 static constexpr uint32_t G1PADD_STRIDE_W = align128w(VM_G1PADD_NSLOTS * 12);
 static constexpr size_t LDS_G1PADD = ((size_t)SLOT_BASE_W + (64 / VM_G1PADD_W) * (size_t)G1PADD_STRIDE_W) * 4;
 static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1024 && LDS_SIGCHK <= 64 * 1024 &&
-                  LDS_PKCHK <= 64 * 1024 && LDS_G1PADD <= 64 * 1024 && LDS_SIGN <= 64 * 1024 &&
+                  LDS_PKCHK <= 64 * 1024 && LDS_G1PADD <= 64 * 1024 && LDS_SIGN <= 64 * 1024 && LDS_PKGEN <= 64 * 1024 &&
                   LDS_VOTE1 <= 64 * 1024 && LDS_FINAL1 <= 64 * 1024 && LDS_VOTEW <= 64 * 1024 && LDS_QCPRE <= 64 * 1024 && LDS_VOTE1H <= 64 * 1024 &&
                   LDS_QCMIL <= 64 * 1024 && VM_G1PADD_NIN == 6,
               "default LDS limit");
@@ -1626,6 +1671,8 @@ static int vm_init(ovh_ctx* c) {
                 VM_VOTE1_OUT, VM_VOTE1_NOUT));
   CHK(vm_upload(c, c->vm_vote_t1, VM_VOTE_T1_CODE, VM_VOTE_T1_NPHASES, VM_VOTE_T1_W, VM_VOTE_T1_NW, VM_VOTE_T1_IN,
                 VM_VOTE_T1_NIN, VM_VOTE_T1_OUT, VM_VOTE_T1_NOUT));
+  CHK(vm_upload(c, c->vm_pkgen, VM_PKGEN_CODE, VM_PKGEN_NPHASES, VM_PKGEN_W, VM_PKGEN_NW, VM_PKGEN_IN, VM_PKGEN_NIN,
+                VM_PKGEN_OUT, VM_PKGEN_NOUT));
   CHK(vm_upload(c, c->vm_vote1h, VM_VOTE1H_CODE, VM_VOTE1H_NPHASES, VM_VOTE1H_W, VM_VOTE1H_NW, VM_VOTE1H_IN,
                 VM_VOTE1H_NIN, VM_VOTE1H_OUT, VM_VOTE1H_NOUT));
   CHK(vm_upload(c, c->vm_vote_t1h, VM_VOTE_T1H_CODE, VM_VOTE_T1H_NPHASES, VM_VOTE_T1H_W, VM_VOTE_T1H_NW, VM_VOTE_T1H_IN,
@@ -2939,7 +2986,7 @@ int ovh_sk_to_pk(ovh_ctx* c, const uint8_t* key, size_t key_len, uint8_t out[48]
   HIPCHK(hipSetDevice(c->device));
   CHK(ensure_in(c, 128));
   HIPCHK(hipMemcpyAsync(c->in_buf, sk.b, 32, hipMemcpyHostToDevice, c->stream));
-  k_sk_to_pk<<<1, WG, 0, c->stream>>>(1, c->in_buf, c->in_buf + 32);
+  k_vm_pkgen<<<1, 64, LDS_PKGEN, c->stream>>>(1, c->vm_pkgen, c->vm_consts, c->in_buf, c->in_buf + 32);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemsetAsync(c->in_buf, 0, 32, c->stream));
   HIPCHK(hipMemcpyAsync(out, c->in_buf + 32, 48, hipMemcpyDeviceToHost, c->stream));
@@ -3718,7 +3765,9 @@ int ovh_sk_to_pk_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sks, uint8_
   if (n == 0) return 0;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  k_sk_to_pk<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, d_sks, d_pks);
+  constexpr uint32_t SL = 64 / VM_PKGEN_W;
+  k_vm_pkgen<<<(uint32_t)((n + SL - 1) / SL), 64, LDS_PKGEN, c->stream>>>((uint32_t)n, c->vm_pkgen, c->vm_consts, d_sks,
+                                                                        d_pks);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;

@@ -355,6 +355,22 @@ def test_aggregate_vm_tree_matches_oracle(cc, golden):
             assert out["v"] == want[1], len(ss)
 
 
+def test_vm_pkgen_edge_scalars(cc):
+    """Public keys on the VM (program pkgen, four 64-bit chunks) through the device batch entry:
+    scalars 1, 2, 3, empty 64-bit chunks, 2^64 +- 1, r - 1 and seeded random ones == the oracle's
+    compressed [k] G1."""
+    import torch
+    import bls12_381 as bls
+    from consensus_overlord_amd import device as dev
+    r = bls.R
+    rng = random.Random(17)
+    ks = [1, 2, 3, 2 ** 64 - 1, 2 ** 64, 2 ** 64 + 1, 2 ** 192, r - 1, r - 2] + [rng.randrange(1, r) for _ in range(23)]
+    sks = torch.from_numpy(np.stack([np.frombuffer(k.to_bytes(32, "big"), dtype=np.uint8) for k in ks])).cuda()
+    got = dev.sk_to_pk_batch(cc.ctx, sks).cpu().numpy()
+    for k, g in zip(ks, got):
+        assert bytes(g) == bls.g1_compress(bls.sk_to_pk(k)), hex(k)
+
+
 def test_vm_sign_edge_scalars(cc):
     """Crypto::sign on the VM (sign0 + 3 x sign1, the scalar as selb bits of four 64-bit
     launches): scalars with empty 64-bit chunks, single bits, r - 1 and random ones, batch and

@@ -247,5 +247,7 @@ def test_percall_programs_on_interpreter(hx, built, golden_votes, any_all):  # n
     mi = {"pk_X": tin["pk_X"], "pk_Y": tin["pk_Y"], "pk_Z": tin["pk_Z"]}
     mi.update({"h%d" % k: q["st:h%d" % k] for k in range(6)})
     mi.update({"g%d" % k: q["st:g%d" % k] for k in range(12)})
+    # pkgen: one 64-bit window chunk from the identity (gen.check runs the four launches vs the oracle)
+    run("pkgen", {"c0": 0, "c1": 1, "c2": 0}, 0xFEDCBA9876543210)
     o = run("qcmil", mi)
     assert run("final1", {"f%d" % j: o["st:f%d" % j] for j in range(12)}) == {"ok": 1}

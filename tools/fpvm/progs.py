@@ -427,25 +427,43 @@ def build_g1padd():
     return p
 
 
-def _smul64(a, acc, T, first=False):
+def _smul64(a, acc, T, first=False, F="f2"):
     """acc -> [2^64] acc + [k] H over the launch scalar's 64 bits k, 2-bit windows MSB first:
     two doublings and one complete addition of T[v] (T = H, 2H, 3H; v = 0 adds the identity,
-    picked by two selb levels off the doubling chain)."""
+    picked by two selb levels off the doubling chain). F: "f2" (G2, sign) or "fp" (G1, pkgen)."""
     H, H2, H3 = T
-    p = a.p
-    O = ((p.zero, p.zero), (p.one, p.zero), (p.zero, p.zero))
+    O = a.pt_inf(F)
     for w in range(31, -1, -1):
         # the window's addend is selected once the previous window's sum exists
-        dep = None if (first and w == 31) else acc[2][0]
-        lo = a.pt_selb("f2", 2 * w, O, H, dep)
-        hi = a.pt_selb("f2", 2 * w, H2, H3, dep)
-        ad = a.pt_selb("f2", 2 * w + 1, lo, hi, dep)
+        dep = None if (first and w == 31) else (acc[2] if F == "fp" else acc[2][0])
+        lo = a.pt_selb(F, 2 * w, O, H, dep)
+        hi = a.pt_selb(F, 2 * w, H2, H3, dep)
+        ad = a.pt_selb(F, 2 * w + 1, lo, hi, dep)
         if first and w == 31:
             acc = ad
             continue
-        acc = a.pt_dbl("f2", a.pt_dbl("f2", acc))
-        acc = a.pt_add("f2", acc, ad)
+        acc = a.pt_dbl(F, a.pt_dbl(F, acc))
+        acc = a.pt_add(F, acc, ad)
     return acc
+
+
+PKGEN_ACC = ["c0", "c1", "c2"]
+
+
+def build_pkgen():
+    """Public key from a secret scalar (ConsensusCrypto::new, ovh_sk_to_pk): acc -> [2^64] acc +
+    [k] G1 over the launch scalar's 64 bits, 2-bit windows over the constants G1, 2 G1, 3 G1;
+    run four times from the identity (k the scalar's 64-bit chunks, most significant first), the
+    secret only as selb bits."""
+    p = Prog("pkgen")
+    a = Alg(p, use_sop=USE_SOP)
+    G = (p.const(G1X), p.const(G1Y), p.one)
+    G2 = a.pt_dbl("fp", G)        # constants: the IR folds operations on constants
+    G3 = a.pt_add("fp", G2, G)
+    acc = tuple(p.input(n) for n in PKGEN_ACC)
+    for name, v in zip(PKGEN_ACC, _smul64(a, acc, (G, G2, G3), F="fp")):
+        p.output(name, v)
+    return p
 
 
 SIGN0_IN = ["u00", "u01", "u10", "u11"]
@@ -538,6 +556,7 @@ PROGRAMS["pkchk"] = (build_pkchk, PKCHK_IN, PKCHK_OUT)
 PROGRAMS["vote1"] = (build_vote1(False), VOTE_IN, VOTE_OUT)
 PROGRAMS["vote_t1"] = (build_vote1(True), VOTE_T_IN, VOTE_T_OUT)
 PROGRAMS["final1"] = (build_final1, f12_names("f"), ["ok"])
+PROGRAMS["pkgen"] = (build_pkgen, PKGEN_ACC, PKGEN_ACC)
 PROGRAMS["vote1h"] = (build_vote1h(False), VOTE1H_IN, VOTE1H_OUT)
 PROGRAMS["vote_t1h"] = (build_vote1h(True), VOTE_T1H_IN, VOTE_T1H_OUT)
 PROGRAMS["qcpre"] = (build_qcpre, QCPRE_IN, QCPRE_OUT)
