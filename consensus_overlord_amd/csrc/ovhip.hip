@@ -3180,11 +3180,76 @@ static int sum_pks(ovh_ctx* c, const uint8_t* pks, const size_t* pk_lens, size_t
   return 0;
 }
 
+// One homogeneous projective G1 point (planes X, Y, Z at index u) -> 48-byte compressed encoding.
+__global__ __launch_bounds__(64) void k_g1p_compress(Slab pts, uint32_t u, uint8_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  Fp X, Y, Z, zz;
+  pts.ld(X, 0, u);
+  pts.ld(Y, 1, u);
+  pts.ld(Z, 2, u);
+  G1J j;  // (X : Y : Z) homogeneous = (X Z : Y Z^2 : Z) Jacobian
+  fp_mul(j.X, X, Z);
+  fp_sqr(zz, Z);
+  fp_mul(j.Y, Y, zz);
+  j.Z = Z;
+  g1_compress(out, j);
+}
+
+// BlsPublicKey::aggregate (consensus.rs:371, 441-443) over compressed keys on the VM: every key
+// decoded by k_vm_pkchk (a key that does not parse -> "lose public key"; the aggregate, like the
+// one-lane path, does not require the subgroup), summed by a g1padd tree, compressed. Returns 1
+// when the one-lane path must decide (other encodings, no keys).
+static int aggregate_pks_vm(ovh_ctx* c, const uint8_t* pks, const size_t* pk_lens, size_t n, uint8_t* out48) {
+  if (n == 0) return 1;
+  for (size_t i = 0; i < n; ++i)
+    if (pk_lens[i] != 48) return 1;
+  if (2 * n > c->qt_cap || !c->qt_buf) {  // keys in [0, n), the tree's levels ping-pong over [0, 2n)
+    if (c->qt_buf) (void)hipFree(c->qt_buf);
+    c->qt_buf = nullptr;
+    c->qt_cap = 0;
+    uint32_t cap = 64;
+    while (cap < 2 * n) cap <<= 1;
+    HIPCHK(hipMalloc(&c->qt_buf, (size_t)(3 * 12 + 1) * cap * 4));
+    c->qt_cap = cap;
+  }
+  CHK(ensure_in(c, n * 48 + 64));
+  uint8_t* d = c->in_buf;  // keys | compressed sum
+  HIPCHK(hipMemcpyAsync(d, pks, n * 48, hipMemcpyHostToDevice, c->stream));
+  uint32_t* kflags = c->qt_buf + (size_t)3 * 12 * c->qt_cap;
+  constexpr uint32_t PK_SL = 64 / VM_PKCHK_W;
+  k_vm_pkchk<<<(uint32_t)((n + PK_SL - 1) / PK_SL), 64, LDS_PKCHK, c->stream>>>((uint32_t)n, c->vm_pkchk, c->vm_consts, d,
+                                                                               Slab{c->qt_buf, c->qt_cap}, kflags);
+  HIPCHK(hipGetLastError());
+  std::vector<uint32_t> hf(n);
+  HIPCHK(hipMemcpyAsync(hf.data(), kflags, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < n; ++i)
+    if (hf[i] & PKF_PARSE) return OVH_ERR_PUBKEY;
+  constexpr uint32_t SL = 64 / VM_G1PADD_W;
+  uint32_t m = (uint32_t)n, base = 0;
+  while (m > 1) {
+    const uint32_t half = (m + 1) / 2, dst = base ? 0 : (uint32_t)n;
+    k_vm_g1tree<<<(half + SL - 1) / SL, 64, LDS_G1PADD, c->stream>>>(m, c->vm_g1padd, G1PADD_STRIDE_W, c->vm_consts,
+                                                                     Slab{c->qt_buf + base, c->qt_cap},
+                                                                     Slab{c->qt_buf + dst, c->qt_cap});
+    m = half;
+    base = dst;
+  }
+  uint8_t* o48 = d + ((n * 48 + 15) & ~(size_t)15);
+  k_g1p_compress<<<1, 64, 0, c->stream>>>(Slab{c->qt_buf + base, c->qt_cap}, 0, o48);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(out48, o48, 48, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
 int ovh_aggregate_pks(ovh_ctx* c, const uint8_t* pks, const size_t* pk_lens, size_t n, uint8_t out[48]) {
-  if (!c || !out) return OVH_ERR_ARG;
+  if (!c || !out || (n && (!pks || !pk_lens))) return OVH_ERR_ARG;
   c = pick_sub(c);
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
+  const int r = aggregate_pks_vm(c, pks, pk_lens, n, out);
+  if (r != 1) return r;
   uint32_t* sum = nullptr;
   return sum_pks(c, pks, pk_lens, n, 0, out, &sum);
 }

@@ -76,3 +76,29 @@ def test_validator_table_golden_keys(golden):
     want = [orc.verify_aggregated(s, hh, v) for s, hh, v in qcs]
     assert got.tolist() == want
     assert want[0] == 0 and want[2] == 0
+
+
+def test_aggregate_pks_vm_matches_oracle(golden):
+    """BlsPublicKey::aggregate on the VM (pkchk + g1padd tree + compression): sizes 1 .. 300,
+    repeated keys, a key and its negation, every 48-byte golden key case (infinity, outside G1,
+    unparseable -> 102) alone and inside a list, against the C oracle (bytes and codes)."""
+    import consensus_overlord_amd as coa
+    import orc
+    c = coa.ConsensusCrypto(bytes.fromhex("3d" * 32))
+    _, _, pks = sv.make(c.ctx, 300, lo=60000)
+    pks = [bytes(p) for p in pks]
+    neg = sv.bls.g1_compress(sv.bls.pt_neg(sv.bls.FpOps, sv.bls.g1_from_bytes(pks[3])))
+    lists = [pks[:n] for n in (1, 2, 3, 67, 100, 129, 300)]
+    lists += [pks[:1] + pks[:1], pks[:40] + pks[:40], pks[:5] + [neg] + pks[3:4]]
+    for x in golden["verify"]:
+        if len(x["pk"]) == 96:
+            lists.append([bytes.fromhex(x["pk"])])
+            lists.append(pks[:3] + [bytes.fromhex(x["pk"])] + pks[3:5])
+    for voters in lists:
+        code, want = orc.aggregate_pks(voters)
+        out = ctypes.create_string_buffer(48)
+        got = c.lib.ovh_aggregate_pks(c.ctx.ptr, b"".join(voters),
+                                      (ctypes.c_size_t * len(voters))(*[len(v) for v in voters]), len(voters), out)
+        assert got == code, (len(voters), got, code)
+        if code == 0:
+            assert out.raw == want, len(voters)
