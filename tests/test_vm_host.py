@@ -206,8 +206,8 @@ def test_fp_inv(hx):
 @pytest.mark.parametrize("any_all", [0, 1])
 def test_percall_programs_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
     """The per-call programs through the interpreter == simulator: sigchk / pkchk on golden
-    signatures and keys (a non-subgroup case included), g1padd, sign0 + sign1 over a golden
-    key's scalar chunks, vote1 / vote_t1 + final1 and the small-batch votew / votew_t + final1 on a
+    signatures and keys (a non-subgroup case included), g1padd, signg0 + signg1 over a golden
+    key's GLS digits, vote1 / vote_t1 + final1 and the small-batch votew / votew_t + final1 on a
     golden vote (gen.check ties each to
     the oracle: decompressed points, sums, the golden signature, the pairing verdict)."""
     consts, progs_ = built
@@ -226,10 +226,10 @@ def test_percall_programs_on_interpreter(hx, built, golden_votes, any_all):  # n
     A, B = (bls.g1_from_bytes(bytes.fromhex(k["pk"])) for k in g["keys"][:2])
     run("g1padd", dict(zip(progs.G1A_IN + progs.G1B_IN, [A[0] * 3 % P, A[1] * 3 % P, 3, B[0], B[1], 1])))
     sk = int(g["keys"][0]["sk"], 16)
-    chunks = [(sk >> (64 * j)) & (2 ** 64 - 1) for j in (3, 2, 1, 0)]
+    d = gen.gls_digits(sk)
     inp = golden_votes[0]
-    o = run("sign0", {n: inp[n] for n in progs.SIGN0_IN}, chunks[0])
-    run("sign1", {n: o[n] for n in progs.SIGN_ACC + progs.SIGN_H}, chunks[1])
+    o = run("signg0", {n: inp[n] for n in progs.SIGN0_IN}, gen.signg_scalar(d, 0))
+    run("signg1", {n: o[n] for n in progs.SIGN_ACC + progs.SIGNG_T}, gen.signg_scalar(d, 1))
     o = run("vote1", inp, 1)
     fin = {"f%d" % j: o["st:f%d" % j] for j in range(12)}
     assert run("final1", fin) == {"ok": 1}

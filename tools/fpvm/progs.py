@@ -21,9 +21,11 @@ layouts. Input and output names are listed in the order the HIP side addresses t
   pkchk    a public key's decompression + G1 subgroup check (the validator table and the keys of
            verify_aggregated_signature), affine key out
   g1padd   A + B in G1 (projective): the pairwise tree that sums an aggregated key
-  sign0    Crypto::sign, first part: H = hash_to_G2(u0, u1), then [k]H for the top 64 bits k of
-           the secret scalar (selb on the launch's scalar: the schedule does not depend on it)
-  sign1    acc -> [2^64] acc + [k] H for the next 64 bits (run three times)
+  signg0   Crypto::sign, first part: H = hash_to_G2(u0, u1), the 15 sums of [|x|^i] H (GLS),
+           the first 16 steps of the 4-digit chain (selb on the launch's scalar: the schedule
+           does not depend on the secret)
+  signg1   the next 16 chain steps (run three times)
+  pkgen    acc -> [2^64] acc + [k] G1 over a 64-bit chunk k of a secret scalar (run four times)
   fold     4 partials (F_i in Fp12, S_i projective G2) -> (prod F_i, sum S_i)
   final    up to 4 partials -> prod F * Miller(-G1, sum S) -> final exponentiation == 1; also
            the bisection checks of the fallback (one group's partial, or one vote's (f, r sigma):
@@ -427,24 +429,78 @@ def build_g1padd():
     return p
 
 
-def _smul64(a, acc, T, first=False, F="f2"):
+def _smul64(a, acc, T, F="fp"):
     """acc -> [2^64] acc + [k] H over the launch scalar's 64 bits k, 2-bit windows MSB first:
     two doublings and one complete addition of T[v] (T = H, 2H, 3H; v = 0 adds the identity,
-    picked by two selb levels off the doubling chain). F: "f2" (G2, sign) or "fp" (G1, pkgen)."""
+    picked by two selb levels off the doubling chain). F: "fp" (G1, pkgen) or "f2" (G2)."""
     H, H2, H3 = T
     O = a.pt_inf(F)
     for w in range(31, -1, -1):
         # the window's addend is selected once the previous window's sum exists
-        dep = None if (first and w == 31) else (acc[2] if F == "fp" else acc[2][0])
+        dep = acc[2] if F == "fp" else acc[2][0]
         lo = a.pt_selb(F, 2 * w, O, H, dep)
         hi = a.pt_selb(F, 2 * w, H2, H3, dep)
         ad = a.pt_selb(F, 2 * w + 1, lo, hi, dep)
-        if first and w == 31:
-            acc = ad
-            continue
         acc = a.pt_dbl(F, a.pt_dbl(F, acc))
         acc = a.pt_add(F, acc, ad)
     return acc
+
+
+SIGNG_T = ["t%d" % k for k in range(90)]   # T[b] = sum of B_i over the set bits i of b, b = 1..15
+
+
+def _signg_steps(a, acc, T, first=False):
+    """16 steps of the 4-dimensional GLS chain acc -> 2 acc + T[b], b = the step's 4 selb bits
+    (bit 4t + i of the launch scalar: digit i at this step), MSB first; T[0] = O."""
+    tab = [a.pt_inf("f2")] + T
+    for t in range(15, -1, -1):
+        dep = None if (first and t == 15) else acc[2][0]
+        lv = tab
+        for i in range(4):   # selb tree: digit i picks between the entries with bit i clear / set
+            lv = [a.pt_selb("f2", 4 * t + i, lv[2 * m], lv[2 * m + 1], dep) for m in range(len(lv) // 2)]
+        ad = lv[0]
+        acc = ad if (first and t == 15) else a.pt_add("f2", a.pt_dbl("f2", acc), ad)
+    return acc
+
+
+def _gls_table(a, H):
+    """B_i = [|x|^i] H = (-psi)^i (H) on G2 (psi acts as x < 0), and T[b] = sum_{i in b} B_i."""
+    B1 = a.pt_neg("f2", a.g2_psi(H))
+    B2 = a.g2_psi(a.g2_psi(H))
+    B3 = a.pt_neg("f2", a.g2_psi(B2))
+    B = [H, B1, B2, B3]
+    T = {0: None}
+    for b in range(1, 16):
+        low = b & (b - 1)          # b without its top set bit
+        top = B[(b ^ low).bit_length() - 1]
+        T[b] = top if low == 0 else a.pt_add("f2", T[low], top)
+    return [T[b] for b in range(1, 16)]
+
+
+def build_signg0():
+    """Crypto::sign by the 4-dimensional GLS decomposition k = sum k_i |x|^i (k_i < 2^64): H =
+    hash_to_G2(u0, u1), the 15-entry table of sums of [|x|^i] H, and the first 16 of the 64 chain
+    steps (digit bits 63..48); the secret enters only as selb bits."""
+    p = Prog("signg0")
+    a = Alg(p, use_sop=USE_SOP)
+    H = a.hash_to_g2((p.input("u00"), p.input("u01")), (p.input("u10"), p.input("u11")))
+    T = _gls_table(a, H)
+    acc = _signg_steps(a, None, T, first=True)
+    flat_t = [c for pt in T for c in flat_g2p(pt)]
+    for name, v in zip(SIGN_ACC + SIGNG_T, flat_g2p(acc) + flat_t):
+        p.output(name, v)
+    return p
+
+
+def build_signg1():
+    """The next 16 GLS chain steps (run three times)."""
+    p = Prog("signg1")
+    a = Alg(p, use_sop=USE_SOP)
+    acc = _pt_in(p, SIGN_ACC)
+    T = [unflat_g2p([p.input(n) for n in SIGNG_T[6 * j:6 * j + 6]]) for j in range(15)]
+    for name, v in zip(SIGN_ACC, flat_g2p(_signg_steps(a, acc, T))):
+        p.output(name, v)
+    return p
 
 
 PKGEN_ACC = ["c0", "c1", "c2"]
@@ -468,30 +524,6 @@ def build_pkgen():
 
 SIGN0_IN = ["u00", "u01", "u10", "u11"]
 SIGN_ACC = ["c%d" % k for k in range(6)]
-SIGN_H = ["h%d" % k for k in range(18)]   # H, 2H, 3H (projective)
-
-
-def build_sign0():
-    p = Prog("sign0")
-    a = Alg(p, use_sop=USE_SOP)
-    H = a.hash_to_g2((p.input("u00"), p.input("u01")), (p.input("u10"), p.input("u11")))
-    H2 = a.pt_dbl("f2", H)
-    H3 = a.pt_add("f2", H2, H)
-    O = ((p.zero, p.zero), (p.one, p.zero), (p.zero, p.zero))
-    acc = _smul64(a, O, (H, H2, H3), first=True)
-    for name, v in zip(SIGN_ACC + SIGN_H, flat_g2p(acc) + flat_g2p(H) + flat_g2p(H2) + flat_g2p(H3)):
-        p.output(name, v)
-    return p
-
-
-def build_sign1():
-    p = Prog("sign1")
-    a = Alg(p, use_sop=USE_SOP)
-    acc = _pt_in(p, SIGN_ACC)
-    T = tuple(unflat_g2p([p.input(n) for n in SIGN_H[6 * j:6 * j + 6]]) for j in range(3))
-    for name, v in zip(SIGN_ACC, flat_g2p(_smul64(a, acc, T))):
-        p.output(name, v)
-    return p
 
 
 FOLD_K = 4
@@ -557,12 +589,12 @@ PROGRAMS["vote1"] = (build_vote1(False), VOTE_IN, VOTE_OUT)
 PROGRAMS["vote_t1"] = (build_vote1(True), VOTE_T_IN, VOTE_T_OUT)
 PROGRAMS["final1"] = (build_final1, f12_names("f"), ["ok"])
 PROGRAMS["pkgen"] = (build_pkgen, PKGEN_ACC, PKGEN_ACC)
+PROGRAMS["signg0"] = (build_signg0, SIGN0_IN, SIGN_ACC + SIGNG_T)
+PROGRAMS["signg1"] = (build_signg1, SIGN_ACC + SIGNG_T, SIGN_ACC)
 PROGRAMS["vote1h"] = (build_vote1h(False), VOTE1H_IN, VOTE1H_OUT)
 PROGRAMS["vote_t1h"] = (build_vote1h(True), VOTE_T1H_IN, VOTE_T1H_OUT)
 PROGRAMS["qcpre"] = (build_qcpre, QCPRE_IN, QCPRE_OUT)
 PROGRAMS["qcmil"] = (build_qcmil, QCMIL_IN, [])
 PROGRAMS["votew"] = (build_votew(False), VOTE_IN, VOTE_OUT)
 PROGRAMS["votew_t"] = (build_votew(True), VOTE_T_IN, VOTE_T_OUT)
-PROGRAMS["sign0"] = (build_sign0, SIGN0_IN, SIGN_ACC + SIGN_H)
-PROGRAMS["sign1"] = (build_sign1, SIGN_ACC + SIGN_H, SIGN_ACC)
 PROGRAMS["g1padd"] = (build_g1padd, G1A_IN + G1B_IN, G1_OUT)
