@@ -1382,9 +1382,55 @@ __global__ __launch_bounds__(64) void k_pack_partial2(Slab F, Slab S, uint32_t* 
 }
 
 // ---- single-call kernels (one lane) ----
-__global__ __launch_bounds__(WG) void k_verify_one(const uint8_t* sig, uint32_t sl, const uint8_t* hash, uint32_t hl, const uint8_t* pk,
-                             uint32_t pl, XmdTemplates t, int32_t* out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) *out = verify_one(sig, sl, hash, hl, pk, pl, t);
+// ovh_verify with other encodings (uncompressed keys / signatures, other lengths): parse them
+// with blst's from_bytes semantics (ec.hpp; an uncompressed point costs an on-curve check, a few
+// products) and write the compressed form of one staged vote, so the vote runs the fixed-size
+// path (vote1 + final1). A parsed point is re-encoded (the compressed path decompresses it to the
+// same point); a failure is replaced by a compressed encoding that fails the same way in the same
+// place: x >= p (BAD_ENCODING; for the key every failure is 102 in verify_one's order, 
+// consensus.rs:406-407), an x with x^3 + 4 (1 + i) not a square (POINT_NOT_ON_CURVE).
+__global__ __launch_bounds__(64) void k_canon_one(const uint8_t* __restrict__ sig, uint32_t sl,
+                                                  const uint8_t* __restrict__ pk, uint32_t pl, uint8_t* __restrict__ sig96,
+                                                  uint8_t* __restrict__ pk48) {
+  if (threadIdx.x != 0) return;
+  if (sl == 96 && (sig[0] & 0x80)) {
+    for (int i = 0; i < 96; ++i) sig96[i] = sig[i];
+  } else {
+    G2A a;
+    bool inf;
+    const int e = g2_from_bytes(a, inf, sig, sl);
+    for (int i = 0; i < 96; ++i) sig96[i] = 0;
+    if (e == BLST_SUCCESS && inf) {
+      sig96[0] = 0xc0;
+    } else if (e == BLST_SUCCESS || e == BLST_POINT_NOT_IN_GROUP) {  // x = 0 (never on E2)
+      fp_to_be48(sig96, a.x.c1);
+      fp_to_be48(sig96 + 48, a.x.c0);
+      sig96[0] |= 0x80 | (fp2_lex_largest(a.y) ? 0x20 : 0);
+    } else if (e == BLST_POINT_NOT_ON_CURVE) {
+      sig96[0] = 0x80;  // x = 1: 5 + 4i is not a square in Fp2
+      sig96[95] = 1;
+    } else {
+      sig96[0] = 0x9f;
+      for (int i = 1; i < 96; ++i) sig96[i] = 0xff;
+    }
+  }
+  if (pl == 48 && (pk[0] & 0x80)) {
+    for (int i = 0; i < 48; ++i) pk48[i] = pk[i];
+  } else {
+    G1A a;
+    bool inf;
+    const int e = g1_from_bytes(a, inf, pk, pl);
+    for (int i = 0; i < 48; ++i) pk48[i] = 0;
+    if (e == BLST_SUCCESS && inf) {
+      pk48[0] = 0xc0;
+    } else if (e == BLST_SUCCESS) {
+      fp_to_be48(pk48, a.x);
+      pk48[0] |= 0x80 | (fp_lex_largest(a.y) ? 0x20 : 0);
+    } else {
+      pk48[0] = 0x9f;
+      for (int i = 1; i < 48; ++i) pk48[i] = 0xff;
+    }
+  }
 }
 
 // Parse list items: code_sig[i] (blst code, group-checked if gc) and the Jacobian point.
@@ -3087,17 +3133,21 @@ int ovh_verify(ovh_ctx* c, const uint8_t* sig, size_t sig_len, const uint8_t* ha
     HIPCHK(hipStreamSynchronize(s->stream));
     return out;
   }
-  // other encodings (uncompressed keys / signatures, wrong lengths): the single-lane kernel
-  CHK(ensure_in(s, 32 + sig_len + pk_len + 64));
+  // other encodings (uncompressed keys / signatures, other lengths): k_canon_one turns them into
+  // one staged compressed vote (sig [0, 96), hash [96, 128), key [128, 176), code at 176; the
+  // raw bytes from 256), which takes the fixed-size path above
+  CHK(ensure_in(s, 256 + sig_len + pk_len + 64));
   uint8_t* d = s->in_buf;
-  HIPCHK(hipMemcpyAsync(d, hash, 32, hipMemcpyHostToDevice, s->stream));
-  if (sig_len) HIPCHK(hipMemcpyAsync(d + 32, sig, sig_len, hipMemcpyHostToDevice, s->stream));
-  if (pk_len) HIPCHK(hipMemcpyAsync(d + 32 + sig_len, pk, pk_len, hipMemcpyHostToDevice, s->stream));
-  k_verify_one<<<1, WG, 0, s->stream>>>(d + 32, (uint32_t)sig_len, d, 32, d + 32 + sig_len, (uint32_t)pk_len, s->xmd,
-                                         s->result);
+  uint8_t* raw = d + 256;
+  HIPCHK(hipMemcpyAsync(d + 96, hash, 32, hipMemcpyHostToDevice, s->stream));
+  if (sig_len) HIPCHK(hipMemcpyAsync(raw, sig, sig_len, hipMemcpyHostToDevice, s->stream));
+  if (pk_len) HIPCHK(hipMemcpyAsync(raw + sig_len, pk, pk_len, hipMemcpyHostToDevice, s->stream));
+  k_canon_one<<<1, 64, 0, s->stream>>>(raw, (uint32_t)sig_len, raw + sig_len, (uint32_t)pk_len, d, d + 128);
   HIPCHK(hipGetLastError());
+  int32_t* dc = (int32_t*)(d + 176);
+  CHK(verify_one_locked(s, d, d + 96, KeySrc{d + 128, PkSrc{}}, dc, hash));
   int32_t r = -1;
-  HIPCHK(hipMemcpyAsync(&r, s->result, 4, hipMemcpyDeviceToHost, s->stream));
+  HIPCHK(hipMemcpyAsync(&r, dc, 4, hipMemcpyDeviceToHost, s->stream));
   HIPCHK(hipStreamSynchronize(s->stream));
   return r;
 }

@@ -372,19 +372,27 @@ def test_vm_pkgen_edge_scalars(cc):
 
 
 def test_vm_sign_edge_scalars(cc):
-    """Crypto::sign on the VM (sign0 + 3 x sign1, the scalar as selb bits of four 64-bit
-    launches): scalars with empty 64-bit chunks, single bits, r - 1 and random ones, batch and
-    per-call, against the C oracle."""
+    """Crypto::sign on the VM (signg0 + 3 x signg1: the GLS digits of k mod r as selb bits):
+    scalars with empty 64-bit chunks, single bits, r - 1, powers of |x| and their neighbours
+    (digit carries and all-maximal digits), scalars >= r (reduced on the device) and random ones,
+    batch and per-call, against the C oracle."""
     import torch
     import orc
     from consensus_overlord_amd import device as dev
     r = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
     rng = random.Random(0x516)
     ks = [1, 2, 3, 2 ** 64 - 1, 2 ** 64, 2 ** 128 + 1, 2 ** 192, 2 ** 254, r - 1, r - 2 ** 64]
-    ks += [rng.randrange(1, r) for _ in range(54)]
+    x = 0xD201000000010000
+    ks += [x - 1, x, x + 1, x ** 2 - 1, x ** 2, x ** 3 - 1, x ** 3, x ** 3 + x - 1,
+           (x - 1) * (1 + x + x ** 2), (r // x ** 3 - 1) * x ** 3 + (x - 1) * (1 + x + x ** 2),
+           r, r + 1, 2 * r + 5, 2 ** 256 - 1]
+    ks += [rng.randrange(1, r) for _ in range(41)]
     sks = [k.to_bytes(32, "big") for k in ks]
     hs = [hashlib.sha256(b"sign %d" % i).digest() for i in range(len(ks))]
-    want = [orc.sign(sk, h) for sk, h in zip(sks, hs)]
+    # H has order r: [k] H = [k mod r] H (the oracle's key parse takes only 0 < k < r; [r] H is
+    # the point at infinity)
+    want = [orc.sign((k % r).to_bytes(32, "big"), h) if k % r else (0, bytes([0xC0]) + bytes(95))
+            for k, h in zip(ks, hs)]
     assert all(w[0] == 0 for w in want)
     d_sk = torch.from_numpy(np.frombuffer(b"".join(sks), dtype=np.uint8).reshape(-1, 32).copy()).cuda()
     d_h = torch.from_numpy(np.frombuffer(b"".join(hs), dtype=np.uint8).reshape(-1, 32).copy()).cuda()
@@ -394,5 +402,5 @@ def test_vm_sign_edge_scalars(cc):
     from consensus_overlord_amd.crypto import FLAG_SK_RAW, Context
     import consensus_overlord_amd as coa
     ctx = Context(flags=FLAG_SK_RAW)
-    for i in (0, 4, 8, 9, 20):
+    for i in (0, 4, 8, 9, 11, 19):
         assert coa.ConsensusCrypto(sks[i], ctx=ctx).sign(hs[i]) == want[i][1], ks[i]
