@@ -1389,71 +1389,77 @@ __global__ __launch_bounds__(64) void k_pack_partial2(Slab F, Slab S, uint32_t* 
 // same point); a failure is replaced by a compressed encoding that fails the same way in the same
 // place: x >= p (BAD_ENCODING; for the key every failure is 102 in verify_one's order, 
 // consensus.rs:406-407), an x with x^3 + 4 (1 + i) not a square (POINT_NOT_ON_CURVE).
+__device__ __noinline__ void canon_sig(const uint8_t* __restrict__ sig, uint32_t sl, uint8_t* __restrict__ sig96) {
+  if (sl == 96 && (sig[0] & 0x80)) {
+    for (int i = 0; i < 96; ++i) sig96[i] = sig[i];
+    return;
+  }
+  G2A a;
+  bool inf;
+  const int e = g2_from_bytes(a, inf, sig, sl);
+  for (int i = 0; i < 96; ++i) sig96[i] = 0;
+  if (e == BLST_SUCCESS && inf) {
+    sig96[0] = 0xc0;
+  } else if (e == BLST_SUCCESS || e == BLST_POINT_NOT_IN_GROUP) {  // x = 0 (never on E2)
+    fp_to_be48(sig96, a.x.c1);
+    fp_to_be48(sig96 + 48, a.x.c0);
+    sig96[0] |= 0x80 | (fp2_lex_largest(a.y) ? 0x20 : 0);
+  } else if (e == BLST_POINT_NOT_ON_CURVE) {
+    sig96[0] = 0x80;  // x = 1: 5 + 4i is not a square in Fp2
+    sig96[95] = 1;
+  } else {
+    sig96[0] = 0x9f;
+    for (int i = 1; i < 96; ++i) sig96[i] = 0xff;
+  }
+}
+
+__device__ __noinline__ void canon_pk(const uint8_t* __restrict__ pk, uint32_t pl, uint8_t* __restrict__ pk48) {
+  if (pl == 48 && (pk[0] & 0x80)) {
+    for (int i = 0; i < 48; ++i) pk48[i] = pk[i];
+    return;
+  }
+  G1A a;
+  bool inf;
+  const int e = g1_from_bytes(a, inf, pk, pl);
+  for (int i = 0; i < 48; ++i) pk48[i] = 0;
+  if (e == BLST_SUCCESS && inf) {
+    pk48[0] = 0xc0;
+  } else if (e == BLST_SUCCESS) {
+    fp_to_be48(pk48, a.x);
+    pk48[0] |= 0x80 | (fp_lex_largest(a.y) ? 0x20 : 0);
+  } else {
+    pk48[0] = 0x9f;
+    for (int i = 1; i < 48; ++i) pk48[i] = 0xff;
+  }
+}
+
 __global__ __launch_bounds__(64) void k_canon_one(const uint8_t* __restrict__ sig, uint32_t sl,
                                                   const uint8_t* __restrict__ pk, uint32_t pl, uint8_t* __restrict__ sig96,
                                                   uint8_t* __restrict__ pk48) {
   if (threadIdx.x != 0) return;
-  if (sl == 96 && (sig[0] & 0x80)) {
-    for (int i = 0; i < 96; ++i) sig96[i] = sig[i];
-  } else {
-    G2A a;
-    bool inf;
-    const int e = g2_from_bytes(a, inf, sig, sl);
-    for (int i = 0; i < 96; ++i) sig96[i] = 0;
-    if (e == BLST_SUCCESS && inf) {
-      sig96[0] = 0xc0;
-    } else if (e == BLST_SUCCESS || e == BLST_POINT_NOT_IN_GROUP) {  // x = 0 (never on E2)
-      fp_to_be48(sig96, a.x.c1);
-      fp_to_be48(sig96 + 48, a.x.c0);
-      sig96[0] |= 0x80 | (fp2_lex_largest(a.y) ? 0x20 : 0);
-    } else if (e == BLST_POINT_NOT_ON_CURVE) {
-      sig96[0] = 0x80;  // x = 1: 5 + 4i is not a square in Fp2
-      sig96[95] = 1;
-    } else {
-      sig96[0] = 0x9f;
-      for (int i = 1; i < 96; ++i) sig96[i] = 0xff;
-    }
-  }
-  if (pl == 48 && (pk[0] & 0x80)) {
-    for (int i = 0; i < 48; ++i) pk48[i] = pk[i];
-  } else {
-    G1A a;
-    bool inf;
-    const int e = g1_from_bytes(a, inf, pk, pl);
-    for (int i = 0; i < 48; ++i) pk48[i] = 0;
-    if (e == BLST_SUCCESS && inf) {
-      pk48[0] = 0xc0;
-    } else if (e == BLST_SUCCESS) {
-      fp_to_be48(pk48, a.x);
-      pk48[0] |= 0x80 | (fp_lex_largest(a.y) ? 0x20 : 0);
-    } else {
-      pk48[0] = 0x9f;
-      for (int i = 1; i < 48; ++i) pk48[i] = 0xff;
-    }
-  }
+  canon_sig(sig, sl, sig96);
+  canon_pk(pk, pl, pk48);
 }
 
-// Parse list items: code_sig[i] (blst code, group-checked if gc) and the Jacobian point.
-__global__ __launch_bounds__(WG) void k_parse_sig_list(uint32_t n, const uint8_t* __restrict__ data,
+// verify_aggregated_signature with other encodings: key i re-encoded to out[48 i, 48 i + 48),
+// the signature to out[48 n, 48 n + 96) (one lane per item).
+__global__ __launch_bounds__(WG) void k_canon_qc(uint32_t n, const uint8_t* __restrict__ data,
+                                                 const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+                                                 const uint8_t* __restrict__ sig, uint32_t sl, uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i < n) canon_pk(data + off[i], (uint32_t)len[i], out + (size_t)48 * i);
+  if (i == n) canon_sig(sig, sl, out + (size_t)48 * n);
+}
+
+// ovh_aggregate_sigs over a list with other encodings: item i re-encoded to out[96 i, 96 i + 96)
+// (one lane per item), then the list runs k_vm_sigchk as a compressed one; offs[i] = 96 i.
+__global__ __launch_bounds__(WG) void k_canon_sig_list(uint32_t n, const uint8_t* __restrict__ data,
                                                        const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
-                                                       int gc, int32_t* __restrict__ codes, Slab pts) {
+                                                       uint8_t* __restrict__ out, uint64_t* __restrict__ offs) {
   const uint32_t i = blockIdx.x * WG + threadIdx.x;
   if (i >= n) return;
-  G2A a;
-  bool inf;
-  int e = g2_from_bytes(a, inf, data + off[i], (uint32_t)len[i]);
-  G2J j;
-  if (e == BLST_SUCCESS) {
-    if (inf) {
-      jac_set_inf(j);
-    } else {
-      jac_from_aff(j, a);
-      if (gc && !g2_in_subgroup(j)) e = GROUPCHECK_FAIL;  // reported after all parses
-    }
-  }
-  if (e != BLST_SUCCESS) jac_set_inf(j);
-  pts.st_g2j(j, i);
-  codes[i] = e;
+  canon_sig(data + off[i], (uint32_t)len[i], out + (size_t)96 * i);
+  offs[i] = (uint64_t)96 * i;
 }
 
 __global__ __launch_bounds__(WG) void k_parse_pk_list(uint32_t n, const uint8_t* __restrict__ data,
@@ -1478,17 +1484,6 @@ __global__ __launch_bounds__(WG) void k_parse_pk_list(uint32_t n, const uint8_t*
   pts.st(Y, 1, i);
   pts.st(Z, 2, i);
   codes[i] = e;
-}
-
-__global__ __launch_bounds__(WG) void k_sum_g2_compress(uint32_t n, Slab pts, uint8_t* out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  G2J acc, x;
-  jac_set_inf(acc);
-  for (uint32_t i = 0; i < n; ++i) {
-    pts.ld_g2j(x, i);
-    jac_add(acc, acc, x);
-  }
-  g2_compress(out, acc);
 }
 
 __global__ __launch_bounds__(WG) void k_sum_g1(uint32_t n, Slab pts, uint32_t* out_jac /*36 words*/, uint8_t* out48) {
@@ -3193,17 +3188,28 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
   c = pick_sub(c);
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  // compressed signatures go through the VM (k_vm_sigchk + a padd tree, planes [0, 2n) of scr);
-  // lists with other encodings through the one-lane parse and sum
-  bool vm_path = n > 0;
-  for (size_t i = 0; i < n; ++i) vm_path = vm_path && sig_lens[i] == 96;
-  CHK(ensure_scr(c, vm_path ? 2 * n : (n > 0 ? n : 1)));
-  CHK(ensure_in(c, list_bytes(sig_lens, n) + list_bytes(pk_lens, n) + 512 + 32 * (n + 1)));
+  // the signatures go through the VM (k_vm_sigchk + a padd tree, planes [0, 2n) of scr); a list
+  // with other encodings (uncompressed, other lengths) is re-encoded first (k_canon_sig_list:
+  // every item as 96 compressed bytes that parse to the same point or fail with the same code)
+  bool compressed = true;
+  for (size_t i = 0; i < n; ++i) compressed = compressed && sig_lens[i] == 96;
+  const size_t canon_bytes = compressed ? 0 : (size_t)104 * n + 64;
+  CHK(ensure_scr(c, n > 0 ? 2 * n : 1));
+  CHK(ensure_in(c, list_bytes(sig_lens, n) + list_bytes(pk_lens, n) + 512 + 32 * (n + 1) + canon_bytes));
   uint8_t *ds, *dp;
   uint64_t *so, *sl, *po, *pl;
   size_t used1 = 0, used2 = 0;
   CHK(stage_list(c, sigs, sig_lens, n, 0, &ds, &so, &sl, &used1));
   CHK(stage_list(c, pks, pk_lens, n, used1, &dp, &po, &pl, &used2));
+  if (n && !compressed) {
+    uint8_t* cs = c->in_buf + ((used2 + 15) & ~(size_t)15);
+    uint64_t* co = (uint64_t*)(cs + (size_t)96 * n);
+    k_canon_sig_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, ds, so, sl, cs, co);
+    HIPCHK(hipGetLastError());
+    ds = cs;
+    so = co;
+    used2 = (size_t)((uint8_t*)(co + n) - c->in_buf);
+  }
   Slab pts{c->scr, c->scr_cap};
   Slab ppts{c->scr + (size_t)6 * 12 * c->scr_cap, c->scr_cap};
   if (n) {
@@ -3217,13 +3223,9 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev_x[3], c->xstream));
     const int gc = (c->flags & OVH_FLAG_AGG_NO_GROUPCHECK) ? 0 : 1;
-    if (vm_path) {
-      constexpr uint32_t SL = 64 / VM_SIGCHK_W;
-      k_vm_sigchk<<<(uint32_t)((n + SL - 1) / SL), 64, LDS_SIGCHK, c->stream>>>((uint32_t)n, c->vm_sigchk, c->vm_consts,
-                                                                                ds, so, gc, c->scr_sig, pts);
-    } else {
-      k_parse_sig_list<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, ds, so, sl, gc, c->scr_sig, pts);
-    }
+    constexpr uint32_t SL = 64 / VM_SIGCHK_W;
+    k_vm_sigchk<<<(uint32_t)((n + SL - 1) / SL), 64, LDS_SIGCHK, c->stream>>>((uint32_t)n, c->vm_sigchk, c->vm_consts,
+                                                                              ds, so, gc, c->scr_sig, pts);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_x[3], 0));
   }
@@ -3242,7 +3244,7 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
   if (n == 0) return BLST_AGGR_TYPE_MISMATCH;
   for (size_t i = 0; i < n; ++i)
     if (cs[i] == GROUPCHECK_FAIL) return BLST_POINT_NOT_IN_GROUP;
-  if (vm_path) {
+  {
     constexpr uint32_t SL = 64 / VM_PADD_W;
     uint32_t m = (uint32_t)n, base = 0;
     while (m > 1) {
@@ -3253,8 +3255,6 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
       base = dst;
     }
     k_g2p_compress<<<1, 64, 0, c->stream>>>(Slab{pts.p + base, pts.cap}, c->in_buf + used2);
-  } else {
-    k_sum_g2_compress<<<1, WG, 0, c->stream>>>((uint32_t)n, pts, c->in_buf + used2);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(out, c->in_buf + used2, 96, hipMemcpyDeviceToHost, c->stream));
@@ -3383,12 +3383,13 @@ static int ensure_qc_buf(ovh_ctx* c, size_t nd) {
 // verify_aggregated_signature (consensus.rs:365-382) on the batch kernels: the keys decoded and
 // group-checked on the VM (k_vm_pkchk), their sum (a g1padd tree), then the vote_t program and
 // the final check for the one (sig, hash, apk). Returns 1 when the exact one-lane path must
-// decide instead (a key outside G1: the sum's own group check decides; other encodings).
+// decide instead (a key outside G1: the sum's own group check decides). Other encodings
+// (uncompressed, other lengths) are re-encoded first (k_canon_qc, as k_canon_one).
 static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_len, const uint8_t* hash,
                                 size_t hash_len, const uint8_t* pks, const size_t* pk_lens, size_t n, int* code) {
-  if (n == 0 || agg_len != 96 || !hash || hash_len != 32) return 1;
-  for (size_t i = 0; i < n; ++i)
-    if (pk_lens[i] != 48) return 1;
+  if (n == 0 || !hash || hash_len != 32 || agg_len > 4096) return 1;
+  bool fixed = agg_len == 96;
+  for (size_t i = 0; i < n; ++i) fixed = fixed && pk_lens[i] == 48;
   if (2 * n > c->qt_cap || !c->qt_buf) {  // keys in [0, n), the tree's levels ping-pong over [0, 2n)
     if (c->qt_buf) (void)hipFree(c->qt_buf);
     c->qt_buf = nullptr;
@@ -3400,12 +3401,24 @@ static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_l
   }
   CHK(ensure_qc_buf(c, 1));
   CHK(ensure_cap(c, 2));
-  CHK(ensure_in(c, n * 48 + 96 + 32 + 64));
+  const size_t raw_base = ((n * 48 + 128 + 15) & ~(size_t)15) + 256;
+  CHK(ensure_in(c, fixed ? n * 48 + 96 + 32 + 64 : raw_base + list_bytes(pk_lens, n) + 16 * (n + 1) + agg_len + 64));
   uint8_t* d = c->in_buf;  // keys | sig | hash | code, qcpre flags
   int32_t* dc = (int32_t*)(d + ((n * 48 + 128 + 15) & ~(size_t)15));
   uint32_t* qpf = (uint32_t*)(dc + 1);
-  HIPCHK(hipMemcpyAsync(d, pks, n * 48, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(d + n * 48, agg_sig, 96, hipMemcpyHostToDevice, c->stream));
+  if (fixed) {
+    HIPCHK(hipMemcpyAsync(d, pks, n * 48, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(d + n * 48, agg_sig, 96, hipMemcpyHostToDevice, c->stream));
+  } else {
+    uint8_t* dp;
+    uint64_t *po, *pl;
+    size_t used = 0;
+    CHK(stage_list(c, pks, pk_lens, n, raw_base, &dp, &po, &pl, &used));
+    uint8_t* rs = c->in_buf + used;
+    if (agg_len) HIPCHK(hipMemcpyAsync(rs, agg_sig, agg_len, hipMemcpyHostToDevice, c->stream));
+    k_canon_qc<<<nblk(n + 1), WG, 0, c->stream>>>((uint32_t)n, dp, po, pl, rs, (uint32_t)agg_len, d);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipMemcpyAsync(d + n * 48 + 96, hash, 32, hipMemcpyHostToDevice, c->stream));
   // the signature's checks, H(m) and Miller(-G1, sigma) on the side stream, beside the keys
   int slot;

@@ -90,3 +90,52 @@ def test_other_encodings_golden_codes(cc, golden):
         if len(h) != 32 or (len(sig) == 96 and len(pk) == 48):
             continue
         assert cc.lib.ovh_verify(cc.ctx.ptr, sig, len(sig), h, len(h), pk, len(pk)) == c["code"], c["name"]
+
+
+def _agg(cc, sigs, pks):
+    import ctypes
+    import orc
+    sd, sl = orc._lens(sigs)
+    pd, pl = orc._lens(pks)
+    out = ctypes.create_string_buffer(96)
+    c = cc.lib.ovh_aggregate_sigs(cc.ctx.ptr, sd, sl, len(sigs), pd, pl, len(pks), out)
+    return c, (out.raw if c == 0 else None)
+
+
+def _vagg(cc, agg, h, pks):
+    import orc
+    pd, pl = orc._lens(pks)
+    return cc.lib.ovh_verify_aggregated(cc.ctx.ptr, agg, len(agg), h, len(h), pd, pl, len(pks))
+
+
+def test_aggregate_and_qc_other_encodings(cc, golden):
+    """aggregate_signatures over lists mixing compressed and uncompressed signatures (and keys),
+    with an off-curve, a bad-length and a non-subgroup item; verify_aggregated_signature with an
+    uncompressed aggregate and uncompressed / odd keys (k_canon_sig_list, k_canon_qc): codes and
+    bytes == the C oracle's."""
+    import bls12_381 as bls
+    import orc
+    q = golden["qc"]
+    pks = [_b(p) for p in q["pks"][:67]]
+    sigs = [_b(s) for s in q["sigs"][:67]]
+    h = _b(q["hash"])
+    su = [bls.g2_serialize(bls.g2_from_bytes(s)) if i % 3 == 0 else s for i, s in enumerate(sigs)]
+    pu = [bls.g1_serialize(bls.g1_from_bytes(p)) if i % 4 == 1 else p for i, p in enumerate(pks)]
+    named = {c["name"]: c for c in golden["verify"]}
+    nig = bls.g2_serialize(bls._g2_uncompress(_b(named["sig_not_in_g2"]["sig"])))
+    off = bytearray(su[0])
+    off[191] ^= 1
+    lists = [(su, pks), (su, pu), (sigs, pu), (su[:5] + [bytes(off)] + su[6:], pks), (su[:6] + [su[6][:100]] + su[7:], pks),
+             (su[:9] + [nig] + su[10:], pks), ([su[0]], [pu[1]])]
+    for s_, p_ in lists:
+        want = orc.aggregate_sigs(s_, p_)
+        assert _agg(cc, s_, p_) == want, want[0]
+    agg = _b(q["agg_sig"])
+    agg_u = bls.g2_serialize(bls.g2_from_bytes(agg))
+    bad_u = bytearray(agg_u)
+    bad_u[191] ^= 1
+    cases = [(agg_u, h, pks), (agg_u, h, pu), (agg, h, pu), (agg_u, h, pu[:66]), (agg_u, _b("00" * 32), pu),
+             (bytes(bad_u), h, pu), (agg_u[:150], h, pu), (agg_u, h, pu[:66] + [pu[1][:60]]),
+             (agg_u, h, pu[:66] + [bls.g1_serialize(None)])]
+    for a, hh, p_ in cases:
+        assert _vagg(cc, a, hh, p_) == orc.verify_aggregated(a, hh, p_), (len(a), len(p_))
