@@ -20,6 +20,11 @@ constexpr uint32_t PINV28 = 0xffcfffdu;  // -p^-1 mod 2^28
 // x = (a << sh) as 14 limbs of 28 bits (a < 2^384 - sh)
 template <int SH>
 __device__ __forceinline__ void split28(uint32_t* x, const uint32_t* a) {
+#if defined(OVH_UBENCH_NOSPLIT)  // microbenchmark only (tools/ubench/vm_phase.hip): wrong values
+#pragma unroll
+  for (int k = 0; k < 14; ++k) x[k] = a[k % 12];
+  return;
+#endif
 #pragma unroll
   for (int k = 0; k < 14; ++k) {
     const int lo = 28 * k - SH;
@@ -37,6 +42,11 @@ __device__ __forceinline__ void split28(uint32_t* x, const uint32_t* a) {
 
 // 14 x 28 -> 12 x 32, then one conditional subtraction (the value is < 2.63 p)
 __device__ __forceinline__ void join28_reduce(uint32_t* r, const uint32_t* t) {
+#if defined(OVH_UBENCH_NOSPLIT)
+#pragma unroll
+  for (int j = 0; j < 12; ++j) r[j] = t[j];
+  return;
+#endif
   uint32_t u[12];
 #pragma unroll
   for (int j = 0; j < 12; ++j) {
