@@ -1057,7 +1057,8 @@ __global__ __launch_bounds__(64) void k_vm_pkgen(uint32_t n, VmDev prog, const u
 // (-psi)^i (H), and one 64-step chain acc -> 2 acc + T[b] over the 15 sums T of those points,
 // b = the four digits' bits at the step (selb: the secret enters only as select bits; launch j
 // takes digit bits 63 - 16 j .. 48 - 16 j, bit 4 t + i of its scalar = bit 48 - 16 j + t of
-// d_i). 2,280 phases against 3,764 for 2-bit windows over the 255-bit scalar (r03s: 4.9 -> 3.5 ms).
+// d_i). 2,123 phases on a 32-lane slice (2,280 at 16 lanes) against 3,764 for 2-bit windows over the
+// 255-bit scalar (r03s: 4.9 -> 3.5 ms).
 constexpr uint64_t X_ABS64 = 0xD201000000010000ull;
 constexpr uint64_t R64[4] = {0xFFFFFFFF00000001ull, 0x53BDA402FFFE5BFEull, 0x3339D80809A1D805ull,
                              0x73EDA753299D7D48ull};
