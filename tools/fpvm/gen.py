@@ -53,9 +53,14 @@ HEAVY_W = {"vote": 64}
 SEC_BIAS = {"vote_t": {"sig": 1500}}
 # programs scheduled without light ops in the idle lanes of product phases (a phase that runs
 # both interpreter blocks costs more than the two apart: r02aa, 997k -> 1,010k verifs/s). The
-# standalone vote1 / vote_t1 (one wave on the GPU) keep mixing and no section bias: 3,167 ->
-# 2,454 phases, cost estimate -18%
-NOMIX = set(filter(None, os.environ.get("OVH_GEN_NOMIX", "vote,vote_t").split(",")))
+# standalone vote1 / vote_t1 (one wave on the GPU) once mixed (r02: 3,167 -> 2,454 phases, cost
+# estimate -18%); r03z A/B on the per-call / small-batch programs, now without mixing (more
+# phases, but no phase of a critical light op pays for a product): verify 4.10 -> 3.93 ms,
+# sign 3.08 -> 3.00, QC 4.41 -> 4.33, config 5 5.8 -> 5.6 ms. The batch final keeps mixing (its
+# slots would outgrow the LDS budget).
+NOMIX = set(filter(None, os.environ.get(
+    "OVH_GEN_NOMIX", "vote,vote_t,vote1,vote_t1,vote1h,vote_t1h,final1,qcpre,qcmil,votew,votew_t,signg0,signg1,"
+    "sigchk,pkchk,pkgen").split(",")))
 # slots: four vote workgroups (4 x 4 slices) and two finals must share a CU's 160 KiB of LDS
 # (ovhip.hip static_assert); vote 159, final 226 slots with these settings
 
