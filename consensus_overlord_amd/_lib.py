@@ -18,6 +18,7 @@ _vp = ctypes.c_void_p
 SIGNATURES = [
     ("ovh_create", _vp, [ctypes.c_int, _u8p, _sz, ctypes.c_uint32]),
     ("ovh_create_multi", _vp, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, _u8p, _sz, ctypes.c_uint32]),
+    ("ovh_multi_peer_matrix", ctypes.c_int, [_vp, _u8p, _sz]),
     ("ovh_destroy", None, [_vp]),
     ("ovh_device_count", ctypes.c_int, [_vp]),
     ("ovh_stream", _vp, [_vp]),

@@ -106,6 +106,14 @@ class Context:
     def device_count(self) -> int:
         return self.lib.ovh_device_count(self.ptr)
 
+    def peer_matrix(self):
+        """ovh_multi_peer_matrix: n x n rows, [a][b] True when device a reaches b's memory
+        directly (xGMI peer access) or a and b are one device."""
+        buf = ctypes.create_string_buffer(64)
+        n = self.lib.ovh_multi_peer_matrix(self.ptr, buf, 64)
+        raise_for(n if n < 0 else 0)
+        return [[bool(buf.raw[a * n + b]) for b in range(n)] for a in range(n)]
+
     def set_test_rlc(self, seed: int, index_base: int = 0) -> None:
         """Tests only (context made with FLAG_TEST_RLC): reproducible batch coefficients."""
         raise_for(self.lib.ovh_set_test_rlc(self.ptr, seed & 0xFFFFFFFFFFFFFFFF, index_base))

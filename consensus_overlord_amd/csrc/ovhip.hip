@@ -999,8 +999,10 @@ __global__ __launch_bounds__(64) void k_g2p_compress(Slab in, uint8_t* out) {
 // significant first; the secret enters only as selb bits), on a 16-lane slice per key, then one
 // lane converts (X : Y : Z) to Jacobian coordinates and compresses (one inversion).
 constexpr uint32_t PKGEN_STRIDE_W = align256w(VM_PKGEN_NSLOTS * 12 + 3 * 12);
+// bl: a uniform random nonzero blinding factor per key (plane 0, host getrandom): the one-lane
+// compression inverts beta Z instead of the secret-dependent Z (its divsteps run variable time)
 __global__ __launch_bounds__(64) void k_vm_pkgen(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
-                                                 const uint8_t* __restrict__ sks, uint8_t* __restrict__ out) {
+                                                 const uint8_t* __restrict__ sks, uint8_t* __restrict__ out, Slab bl) {
   static_assert(VM_PKGEN_NIN == 3 && VM_PKGEN_NOUT == 3, "pkgen program shape (tools/fpvm/progs.py)");
   constexpr uint32_t W = VM_PKGEN_W;
   extern __shared__ uint4 lds4[];
@@ -1036,12 +1038,16 @@ __global__ __launch_bounds__(64) void k_vm_pkgen(uint32_t n, VmDev prog, const u
   }
   k[0] = k[1] = k[2] = k[3] = 0;
   if (active && lane == 0) {
-    Fp X, Y, Z, zz;
+    Fp X, Y, Z, zz, beta;
     for (int l = 0; l < 12; ++l) {
       X.v[l] = acc[l];
       Y.v[l] = acc[12 + l];
       Z.v[l] = acc[24 + l];
     }
+    bl.ld(beta, 0, i);  // (X : Y : Z) = (beta X : beta Y : beta Z)
+    fp_mul(X, X, beta);
+    fp_mul(Y, Y, beta);
+    fp_mul(Z, Z, beta);
     G1J j;  // (X : Y : Z) homogeneous = (X Z : Y Z^2 : Z) Jacobian
     fp_mul(j.X, X, Z);
     fp_sqr(zz, Z);
@@ -1064,23 +1070,19 @@ constexpr uint64_t R64[4] = {0xFFFFFFFF00000001ull, 0x53BDA402FFFE5BFEull, 0x333
                              0x73EDA753299D7D48ull};
 // little-endian 256-bit n -> digits d (n reduced mod r first: n < 2^256 < 3 r)
 __device__ __forceinline__ void gls_digits(uint64_t d[4], uint64_t n[4]) {
+  // branch-free on the secret scalar (no early exit, no data-dependent branch): the
+  // reductions and the long division select by masks
   for (int rep = 0; rep < 2; ++rep) {  // n >= r -> n - r
-    bool ge = true;
-    for (int l = 3; l >= 0; --l) {
-      if (n[l] != R64[l]) {
-        ge = n[l] > R64[l];
-        break;
-      }
+    uint64_t t[4], br = 0;
+    for (int l = 0; l < 4; ++l) {
+      const uint64_t a = n[l], b = R64[l];
+      const uint64_t d1 = a - b;
+      const uint64_t b1 = (uint64_t)(a < b);
+      t[l] = d1 - br;
+      br = b1 | (uint64_t)(d1 < br);
     }
-    if (ge) {
-      uint64_t br = 0;
-      for (int l = 0; l < 4; ++l) {
-        const uint64_t a = n[l], b = R64[l] + br;
-        const uint64_t nb = (b < br) || (a < b) ? 1u : 0u;
-        n[l] = a - b;
-        br = nb;
-      }
-    }
+    const uint64_t keep = 0ull - br;  // all ones when n < r (the subtraction borrowed)
+    for (int l = 0; l < 4; ++l) n[l] = (n[l] & keep) | (t[l] & ~keep);
   }
   for (int i = 0; i < 3; ++i) {  // n /= |x|, d_i = remainder (bit-serial long division)
     uint64_t rem = 0;
@@ -1089,10 +1091,9 @@ __device__ __forceinline__ void gls_digits(uint64_t d[4], uint64_t n[4]) {
       for (int b = 63; b >= 0; --b) {
         const uint64_t top = rem >> 63;
         rem = (rem << 1) | ((n[l] >> b) & 1u);
-        if (top || rem >= X_ABS64) {
-          rem -= X_ABS64;
-          q |= 1ull << b;
-        }
+        const uint64_t ge = top | (uint64_t)(rem >= X_ABS64);
+        rem -= X_ABS64 & (0ull - ge);
+        q |= ge << b;
       }
       n[l] = q;
     }
@@ -1110,8 +1111,11 @@ __device__ __forceinline__ uint64_t signg_scalar(const uint64_t d[4], int j) {
 
 constexpr uint32_t SIGNG_NSLOTS = VM_SIGNG0_NSLOTS > VM_SIGNG1_NSLOTS ? VM_SIGNG0_NSLOTS : VM_SIGNG1_NSLOTS;
 constexpr uint32_t SIGNG_STRIDE_W = align256w(SIGNG_NSLOTS * 12 + 96 * 12 + 8);  // + acc, T stash, digits
+// bl: a uniform random nonzero Fp2 blinding factor per signature (planes 0, 1; host getrandom),
+// multiplied into (X : Y : Z) before the one-lane compression inverts Z (as k_vm_pkgen)
 __global__ __launch_bounds__(64) void k_vm_signg(uint32_t n, VmDev p0, VmDev p1, const uint32_t* __restrict__ cst_g,
-                                                 const uint8_t* __restrict__ sks, Slab s, uint8_t* __restrict__ out) {
+                                                 const uint8_t* __restrict__ sks, Slab s, uint8_t* __restrict__ out,
+                                                 Slab bl) {
   static_assert(VM_SIGNG0_W == VM_SIGNG1_W && VM_SIGNG0_NOUT == 96 && VM_SIGNG1_NIN == 96 && VM_SIGNG1_NOUT == 6,
                 "signg program shapes (tools/fpvm/progs.py)");
   constexpr uint32_t W = VM_SIGNG0_W;
@@ -1180,6 +1184,11 @@ __global__ __launch_bounds__(64) void k_vm_signg(uint32_t n, VmDev p0, VmDev p1,
       Z.c0.v[l] = hst[48 + l];
       Z.c1.v[l] = hst[60 + l];
     }
+    Fp2 beta;
+    bl.ld2(beta, 0, i);
+    fp2_mul(X, X, beta);
+    fp2_mul(Y, Y, beta);
+    fp2_mul(Z, Z, beta);
     G2J j;
     fp2_mul(j.X, X, Z);
     fp2_sqr(zz, Z);
@@ -1629,6 +1638,8 @@ struct ovh_ctx {
   // multi-device (ovh_create_multi): sub-contexts, one per device; the root owns no streams
   std::vector<ovh_ctx*> sub;
   std::atomic<uint32_t> rr{0};
+  std::vector<uint8_t> peer;   // sub.size()^2: peer[a * n + b] = device a reaches b's memory (xGMI)
+  std::vector<int> fin_devs;   // sub indices the pipelined combined check rotates over
   uint8_t* gather = nullptr;  // on sub[0]'s device: ndev x 864 B
   uint32_t* mfin = nullptr;   // on sub[0]'s device: unpack scratch of the gathered partials
   // Pippenger MSM scratch per batch slot (msm.hpp: counts, offsets, level prefixes, sorted
@@ -1660,6 +1671,7 @@ struct ovh_ctx {
   uint64_t hc_hits = 0, hc_misses = 0;
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
+  std::vector<uint32_t> blind_h;  // host copy of the last compression blinds (upload_blinds)
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
   hipEvent_t ev0[OVH_NSTAGES] = {}, ev1[OVH_NSTAGES] = {};
   uint32_t ev_mask = 0;
@@ -2215,9 +2227,10 @@ static int verify_one_locked(ovh_ctx* c, const uint8_t* d_sig, const uint8_t* d_
   if (h_host) {  // the entry is filled in stream order, before any later call can read it
     he = c->hc_next;
     c->hc_next = (c->hc_next + 1) % HC_CAP;
+    // the old entry's planes are about to be overwritten: drop it now; the new key is entered
+    // only once every launch that fills the planes was accepted (below)
     if (!c->hc_keys[he].empty()) c->hc_index.erase(c->hc_keys[he]);
-    c->hc_keys[he] = hk;
-    c->hc_index[hk] = he;
+    c->hc_keys[he].clear();
   }
   k_h2f<<<1, WG, 0, st>>>(1, d_hash, c->xmd, s);
   if (key.bytes)
@@ -2227,6 +2240,12 @@ static int verify_one_locked(ovh_ctx* c, const uint8_t* d_sig, const uint8_t* d_
     k_vm_vote1<true><<<1, 64, LDS_VOTE1, st>>>(c->vm_vote_t1, c->vm_consts, nullptr, key.pts, d_sig, s, d_code,
                                                h_host ? c->hc_inf + he : nullptr);
   if (h_host) k_copy_h<<<1, 64, 0, st>>>(s, hc, he);
+  // a failed launch of k_h2f / vote1 / k_copy_h leaves the entry unregistered
+  HIPCHK(hipGetLastError());
+  if (h_host) {
+    c->hc_keys[he] = hk;
+    c->hc_index[hk] = he;
+  }
   k_vm_final1<<<1, 64, LDS_FINAL1, st>>>(c->vm_final1, c->vm_consts, Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap},
                                           d_code, c->result + RES_BATCH + slot);
   HIPCHK(hipEventRecord(c->ev_back[slot], st));
@@ -2679,7 +2698,8 @@ static int submit_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
   const size_t nd = root->sub.size();
   if (root->hq.size() >= OVH_BATCH_SLOTS) CHK(complete_front(root));
   const int j = (int)(root->hb_k % OVH_BATCH_SLOTS);
-  ovh_ctx* F = root->sub[root->hb_k % nd];
+  // the final device rotates over the devices with peer access to and from all others
+  ovh_ctx* F = root->sub[root->fin_devs.empty() ? 0 : root->fin_devs[root->hb_k % root->fin_devs.size()]];
   ++root->hb_k;
   HostBatch hb;
   hb.codes = codes;
@@ -2894,20 +2914,51 @@ ovh_ctx* ovh_create_multi(const int* devices, int ndev, const uint8_t* dst, size
     }
     root->sub.push_back(s);
   }
-  for (int d = 1; d < ndev; ++d)
-    if (devices[d] != devices[0]) {  // peer access for the partial copies (xGMI); best effort
-      (void)hipSetDevice(devices[0]);
-      (void)hipDeviceEnablePeerAccess(devices[d], 0);
-      (void)hipSetDevice(devices[d]);
-      (void)hipDeviceEnablePeerAccess(devices[0], 0);
+  // Peer access (xGMI) for every ordered pair of distinct devices: the partials go from every
+  // device to the batch's final device, which rotates, and its verdict word back. peer[a][b] = 1
+  // when device a's kernels / copies reach b's memory directly (or a and b are one device); a
+  // pair without it still works (hipMemcpyPeerAsync stages through the host) but is not xGMI.
+  // The final rotates only over devices that reach, and are reached by, every other device.
+  root->peer.assign((size_t)ndev * ndev, 0);
+  for (int a = 0; a < ndev; ++a)
+    for (int b = 0; b < ndev; ++b) {
+      uint8_t ok = 1;
+      if (devices[a] != devices[b]) {
+        int can = 0;
+        ok = 0;
+        if (hipDeviceCanAccessPeer(&can, devices[a], devices[b]) == hipSuccess && can) {
+          (void)hipSetDevice(devices[a]);
+          const hipError_t e = hipDeviceEnablePeerAccess(devices[b], 0);
+          ok = (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) ? 1 : 0;
+        }
+      }
+      root->peer[(size_t)a * ndev + b] = ok;
     }
   (void)hipGetLastError();
+  for (int d = 0; d < ndev; ++d) {
+    bool all = true;
+    for (int e = 0; e < ndev; ++e) all = all && root->peer[(size_t)d * ndev + e] && root->peer[(size_t)e * ndev + d];
+    if (all) root->fin_devs.push_back(d);
+  }
+  if (root->fin_devs.empty()) root->fin_devs.push_back(0);
   if (hipSetDevice(devices[0]) != hipSuccess || hipMalloc(&root->gather, (size_t)16 * OVH_PARTIAL_BYTES) != hipSuccess ||
       hipMalloc(&root->mfin, FIN_STRIDE * 4) != hipSuccess) {
     ovh_destroy(root);
     return nullptr;
   }
   return root;
+}
+
+int ovh_multi_peer_matrix(ovh_ctx* c, uint8_t* out, size_t cap) {
+  if (!c || !out) return OVH_ERR_ARG;
+  const size_t nd = c->sub.empty() ? 1 : c->sub.size();
+  if (cap < nd * nd) return OVH_ERR_ARG;
+  if (c->sub.empty()) {
+    out[0] = 1;
+    return 1;
+  }
+  memcpy(out, c->peer.data(), nd * nd);
+  return (int)nd;
 }
 
 static void destroy_one(ovh_ctx* c) {
@@ -3051,14 +3102,50 @@ int ovh_sk_parse(ovh_ctx* c, const uint8_t* key, size_t key_len, uint8_t out_sca
   return sk_parse(c, key, key_len, out_scalar);
 }
 
+// Blinding factors for the one-lane compressions of k_vm_pkgen / k_vm_signg (their
+// inversion runs variable-time divsteps on a secret-dependent Z): `planes` Fp planes of n
+// uniform nonzero elements below p (getrandom, rejection sampling), uploaded on c->stream into
+// scr planes first..first + planes - 1. Caller holds c->mu and has sized scr for n; the host
+// copy lives in the context until the next call (every caller synchronises before returning).
+static int upload_blinds(ovh_ctx* c, size_t n, uint32_t first, uint32_t planes, Slab* out) {
+  const size_t cap = c->scr_cap;
+  c->blind_h.assign((size_t)planes * 12 * cap, 0u);
+  for (size_t i = 0; i < n; ++i)
+    for (uint32_t j = 0; j < planes; ++j) {
+      uint32_t v[12];
+      for (;;) {
+        size_t got = 0;
+        while (got < sizeof v) {
+          const ssize_t r = getrandom((uint8_t*)v + got, sizeof v - got, 0);
+          if (r < 0) {
+            if (errno == EINTR) continue;
+            return OVH_ERR_RNG;
+          }
+          got += (size_t)r;
+        }
+        v[11] &= 0x1FFFFFFFu;  // p < 2^381: below 2^381, then reject >= p and 0
+        uint32_t z = 0;
+        for (int k = 0; k < 12; ++k) z |= v[k];
+        if (z && limbs_lt_p(v)) break;
+      }
+      for (int k = 0; k < 12; ++k) c->blind_h[((size_t)j * 12 + k) * cap + i] = v[k];
+    }
+  uint32_t* d = c->scr + (size_t)first * 12 * cap;
+  HIPCHK(hipMemcpyAsync(d, c->blind_h.data(), c->blind_h.size() * 4, hipMemcpyHostToDevice, c->stream));
+  *out = Slab{d, (uint32_t)cap};
+  return 0;
+}
+
 // n signatures on c->stream: hash_to_field per hash (k_h2f, u planes in scr), then the VM
 // (k_vm_sign). Caller holds c->mu and has sized scr for n.
 static int enqueue_sign(ovh_ctx* c, size_t n, const uint8_t* d_sks, const uint8_t* d_hashes, uint8_t* d_sigs) {
-  Slab u{c->scr, c->scr_cap};
+  Slab u{c->scr, c->scr_cap}, bl;
+  static_assert(S_U + 4 <= 6, "u planes below the blinding planes");
+  CHK(upload_blinds(c, n, 6, 2, &bl));
   k_h2f<<<nblk(n), WG, 0, c->stream>>>((uint32_t)n, d_hashes, c->xmd, u);
   constexpr uint32_t SL = 64 / VM_SIGNG0_W;
   k_vm_signg<<<(uint32_t)((n + SL - 1) / SL), 64, LDS_SIGNG, c->stream>>>((uint32_t)n, c->vm_signg0, c->vm_signg1,
-                                                                          c->vm_consts, d_sks, u, d_sigs);
+                                                                          c->vm_consts, d_sks, u, d_sigs, bl);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -3091,8 +3178,11 @@ int ovh_sk_to_pk(ovh_ctx* c, const uint8_t* key, size_t key_len, uint8_t out[48]
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   CHK(ensure_in(c, 128));
+  CHK(ensure_scr(c, 1));
+  Slab bl;
+  CHK(upload_blinds(c, 1, 0, 1, &bl));
   HIPCHK(hipMemcpyAsync(c->in_buf, sk.b, 32, hipMemcpyHostToDevice, c->stream));
-  k_vm_pkgen<<<1, 64, LDS_PKGEN, c->stream>>>(1, c->vm_pkgen, c->vm_consts, c->in_buf, c->in_buf + 32);
+  k_vm_pkgen<<<1, 64, LDS_PKGEN, c->stream>>>(1, c->vm_pkgen, c->vm_consts, c->in_buf, c->in_buf + 32, bl);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemsetAsync(c->in_buf, 0, 32, c->stream));
   HIPCHK(hipMemcpyAsync(out, c->in_buf + 32, 48, hipMemcpyDeviceToHost, c->stream));
@@ -3958,9 +4048,12 @@ int ovh_sk_to_pk_batch_device(ovh_ctx* c, size_t n, const uint8_t* d_sks, uint8_
   if (n == 0) return 0;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
+  CHK(ensure_scr(c, n));
+  Slab bl;
+  CHK(upload_blinds(c, n, 0, 1, &bl));
   constexpr uint32_t SL = 64 / VM_PKGEN_W;
   k_vm_pkgen<<<(uint32_t)((n + SL - 1) / SL), 64, LDS_PKGEN, c->stream>>>((uint32_t)n, c->vm_pkgen, c->vm_consts, d_sks,
-                                                                        d_pks);
+                                                                        d_pks, bl);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
   return 0;

@@ -10,11 +10,16 @@ into the library's verdict cache), and only then forwards the messages to overlo
 order. overlord's serial `verify_signature` calls on those messages are answered from the cache
 with the exact per-vote code (hits are counted by `ovh_cache_stats`).
 
-Flush policy: a group that reaches `batch_size` messages (default: the validator count, i.e. a
-full round of votes) flushes everything pending; so does `poll()` once the oldest pending
-message has waited `max_delay_s`. `AggregatedVote` and `SignedProposal` are forwarded at once
-(one aggregated check per QC / one proposal per round: nothing to batch). A message that does
-not decode is dropped with a warning, as the reference does.
+Flush policy: a group that reaches `batch_size` messages flushes everything pending. The
+default is what one round can bring over the network: the validator count minus one when this
+node is a validator (its own vote never crosses the network -- overlord hands it to itself,
+consensus.rs:721-771), else the validator count. A deadline flushes the rest: every arrival
+checks it, and `poll()` -- to be driven by a timer (the node's tokio interval) -- flushes a
+group that stopped growing (offline validators) once its oldest message has waited
+`max_delay_s`. `AggregatedVote` and `SignedProposal` are not batched (one aggregated check per
+QC / one proposal per round); they first flush what is held, so overlord sees every message in
+arrival order, as the reference's proc_network_msg forwards them. A message that does not
+decode is dropped with a warning, as the reference does.
 
 Wire layouts [dep: overlord 0.4 types + rlp 0.5, not vendored; named assumption 7 in DESIGN.md]:
   SignedVote   = rlp([signature bytes, Vote, voter bytes])
@@ -148,10 +153,15 @@ class VoteIngress:
     def _limit(self) -> int:
         if self.batch_size:
             return self.batch_size
-        return max(1, len(getattr(self.crypto, "pubkeys", []) or []) or 256)
+        pks = list(getattr(self.crypto, "pubkeys", []) or [])
+        if not pks:
+            return 256
+        own = getattr(self.crypto, "name", None)
+        return max(1, len(pks) - (1 if own is not None and own in pks else 0))
 
     def proc_network_msg(self, kind: str, payload: bytes) -> None:
         """consensus.rs:210-258 (msg.r#type, msg.msg)."""
+        self.poll()   # the deadline of what is already held
         try:
             if kind == SIGNED_VOTE:
                 m = decode_signed_vote(payload)
@@ -162,6 +172,7 @@ class VoteIngress:
                 self._hold(kind, m, (m.height, m.round, CHOKE_KIND), m.signature, m.address)
                 return
             if kind == AGGREGATED_VOTE or kind == SIGNED_PROPOSAL:
+                self.flush()                # what arrived before goes first (arrival order)
                 self._send(kind, payload)   # decoded by overlord's own types in the node
                 return
         except ValueError as e:

@@ -100,7 +100,14 @@ class ShardVerifier:
 
     def _submit(self, part, sigs, hashes, pks, codes, index_base):
         self.backend.partial(sigs, hashes, pks, codes, part[self.rank], index_base)
-        self._all_gather(part)
+        # the gather runs in the backend's stream order: on the GPU the RCCL collective is
+        # enqueued on the current (gather) stream; a host backend that defers its work to a
+        # stream of its own (the CPU tests' asynchronous oracle) takes the gather as a task
+        enqueue = getattr(self.backend, "enqueue", None)
+        if enqueue is not None:
+            enqueue(lambda: self._all_gather(part))
+        else:
+            self._all_gather(part)
         self.backend.combine_async(part, sigs.shape[0], codes)
 
     def wait(self) -> None:

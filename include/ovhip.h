@@ -64,6 +64,12 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
  * runs the one combined check; on failure every device bisects its own shard. Single-call
  * entry points rotate over the devices. Devices may repeat (tests use {0, 0}); 1 <= ndev <= 8. */
 ovh_ctx* ovh_create_multi(const int* devices, int ndev, const uint8_t* dst, size_t dst_len, uint32_t flags);
+/* Peer access of a context's devices: out[a * n + b] = 1 when device a reaches device b's memory
+ * directly (xGMI; enabled by ovh_create_multi for every pair hipDeviceCanAccessPeer allows) or a
+ * and b are one device, 0 when copies between them stage through the host. Returns n (the
+ * device count), or OVH_ERR_ARG when cap < n * n. The pipelined combined check
+ * (ovh_verify_batch_async) rotates over the devices with peer access to and from every other. */
+int ovh_multi_peer_matrix(ovh_ctx* ctx, uint8_t* out, size_t cap);
 void ovh_destroy(ovh_ctx* ctx);
 /* Number of devices of the context (1 for ovh_create). */
 int ovh_device_count(ovh_ctx* ctx);

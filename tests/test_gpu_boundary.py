@@ -198,3 +198,21 @@ def test_oversized_encodings_keep_reference_precedence(golden):
     assert L.ovh_verify(c.ctx.ptr, big, len(big), h, 32, p, 48) == 1
     assert L.ovh_verify(c.ctx.ptr, big, len(big), h, 32, big, len(big)) == 102
     assert L.ovh_verify(c.ctx.ptr, big, len(big), h, 31, big, len(big)) == 100
+
+
+def test_peer_matrix_of_contexts():
+    """ovh_multi_peer_matrix: a one-device context is its own peer; a context over {0, 0} has
+    every pair on one device (no host staging anywhere); with two GPUs visible, the matrix
+    follows what the runtime reports for the pair."""
+    from consensus_overlord_amd.crypto import Context
+    c = Context()
+    assert c.peer_matrix() == [[True]]
+    m = Context(devices=[0, 0])
+    assert m.peer_matrix() == [[True, True], [True, True]]
+    import torch
+    if torch.cuda.device_count() > 1:   # distinct devices: the matrix is what the runtime allows
+        d = Context(devices=[0, 1])
+        pm = d.peer_matrix()
+        can = torch.cuda.can_device_access_peer(0, 1) and torch.cuda.can_device_access_peer(1, 0)
+        assert pm[0][0] and pm[1][1] and pm[0][1] == torch.cuda.can_device_access_peer(0, 1)
+        assert pm[1][0] == torch.cuda.can_device_access_peer(1, 0) or not can

@@ -184,3 +184,63 @@ def test_ingress_stream_on_device_every_verify_is_a_cache_hit():
     h1, m1, _ = cc.cache_stats()
     assert h1 - h0 == len(fwd) and m1 == m0
     assert nbad == 2 and sh.stats["batches"] >= 1
+
+
+def test_relayer_flushes_at_n_minus_one_without_the_deadline():
+    """A validator never receives its own vote over the network (consensus.rs:721-771): with its
+    name among the validators, a group flushes at N - 1 votes, with no deadline and no poll()."""
+    import orc
+    nval = 5
+    sks = [(int.from_bytes(sm3(b"relayer %d" % i), "big") >> 3).to_bytes(32, "big") for i in range(nval)]
+    pks = [orc.sk_to_pk(k)[1] for k in sks]
+    oc = OracleCrypto(pks)
+    oc.name = pks[0]                                        # this node is validator 0
+    msgs = _stream(nval, 4, 0, sm3(b"block 4"), lambda i, d: orc.sign(sks[i], d)[1], pks)
+    fwd = []
+    sh = ig.VoteIngress(oc, lambda k, m: fwd.append((k, m)), max_delay_s=1e9, clock=lambda: 0.0)
+    others = [(k, m) for k, m in msgs if m.voter != pks[0]]
+    prevotes = [x for x in others if x[1].vote_type == vote.PREVOTE]
+    assert len(prevotes) == nval - 1
+    for k, m in prevotes[:-1]:
+        sh.proc_network_msg(k, ig.encode_signed_vote(m))
+    assert fwd == []
+    sh.proc_network_msg(prevotes[-1][0], ig.encode_signed_vote(prevotes[-1][1]))
+    assert oc.prefetch_calls == [nval - 1] and [m for _, m in fwd] == [m for _, m in prevotes]
+
+
+def test_aggregated_vote_and_proposal_keep_arrival_order():
+    """Held votes are forwarded before an AggregatedVote / SignedProposal that arrives after them."""
+    import orc
+    nval = 4
+    sks = [(int.from_bytes(sm3(b"order %d" % i), "big") >> 3).to_bytes(32, "big") for i in range(nval)]
+    pks = [orc.sk_to_pk(k)[1] for k in sks]
+    oc = OracleCrypto(pks)
+    msgs = _stream(nval, 5, 2, sm3(b"block 5"), lambda i, d: orc.sign(sks[i], d)[1], pks)
+    fwd = []
+    sh = ig.VoteIngress(oc, lambda k, m: fwd.append((k, m)), max_delay_s=1e9, clock=lambda: 0.0)
+    for k, m in msgs[:2]:
+        sh.proc_network_msg(k, ig.encode_signed_vote(m))
+    assert fwd == []
+    sh.proc_network_msg("AggregatedVote", b"qc bytes")
+    assert [k for k, _ in fwd] == ["SignedVote", "SignedVote", "AggregatedVote"]
+    assert oc.prefetch_calls == [2]
+    sh.proc_network_msg(*("SignedVote", ig.encode_signed_vote(msgs[2][1])))
+    sh.proc_network_msg("SignedProposal", b"proposal bytes")
+    assert [k for k, _ in fwd][3:] == ["SignedVote", "SignedProposal"]
+
+
+def test_deadline_checked_on_arrival():
+    """A held group whose oldest message has waited max_delay_s is flushed by the next arrival."""
+    import orc
+    nval = 6
+    sks = [(int.from_bytes(sm3(b"deadline %d" % i), "big") >> 3).to_bytes(32, "big") for i in range(nval)]
+    pks = [orc.sk_to_pk(k)[1] for k in sks]
+    oc = OracleCrypto(pks)
+    msgs = _stream(nval, 6, 0, sm3(b"block 6"), lambda i, d: orc.sign(sks[i], d)[1], pks)
+    fwd = []
+    now = [0.0]
+    sh = ig.VoteIngress(oc, lambda k, m: fwd.append((k, m)), max_delay_s=0.01, clock=lambda: now[0])
+    sh.proc_network_msg("SignedVote", ig.encode_signed_vote(msgs[0][1]))
+    now[0] = 0.05
+    sh.proc_network_msg("SignedVote", ig.encode_signed_vote(msgs[1][1]))
+    assert [m for _, m in fwd] == [msgs[0][1]] and oc.prefetch_calls == [1]
