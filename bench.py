@@ -44,11 +44,15 @@ G2_GEN_COMPRESSED = bytes.fromhex(
     "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8")
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 OVH_FLAG_PROFILE = 0x2
-# measured v_mad_u64_u32 lane-op rate on gfx950 (tools/ubench/int_rates.hip,
-# profiles/r01_int_rates_ubench.json) and the full-rate 32-bit VALU lane rate
-# (256 CU x 4 SIMD x 32 lanes x 2.4 GHz).
+OVH_FLAG_VM_CLOCK = 0x20
+# Roofline denominators (integer VALU):
+#  PEAK_FULLRATE  the theoretical full-rate 32-bit VALU lane rate, 256 CU x 64 lanes/clk x
+#                 2.4 GHz = 3.93e13 lane-ops/s (one wave instruction per 4 cycles per SIMD)
+#  PEAK_MAD_U64   the measured v_mad_u64_u32 lane-op rate (tools/ubench/int_rates.hip, best
+#                 occupancy; profiles/r04_int_rates.json), at the clock that run held
+PEAK_FULLRATE = 256 * 64 * 2.4e9
 PEAK_MAD_U64 = 2.9143e13
-PEAK_FULLRATE = 256 * 4 * 32 * 2.4e9
+PEAK_MAD_U64_CLOCK_GHZ = None
 W_V_CANON = 18300   # algorithmic Montgomery products per verification
 W_MSM = 350         # the Pippenger share of sum r_i sigma_i (the k_msm_* kernels)
 STAGE_TO_WORK = {"hash_to_field": "hash_to_field", "vote": "vote", "fold": "fold_per_partial",
@@ -151,7 +155,14 @@ def latencies(ctx, sigs, hs, pks) -> dict:
       qc67_ms        config 2: verify_aggregated_signature over 67 voters, median of 3
       qc_table_ms    config 2 through the validator table (ovh_verify_qc_batch, one QC)
       cfg5_ms        config 5: 1024 votes with 1% sigma + G2, batch incl. bisection, median of 3
-      cfg5_valid_ms  the same 1024 votes all valid (no bisection)"""
+      cfg5_valid_ms  the same 1024 votes all valid (no bisection)
+      samemsg4096_ms the 4096 config-3 keys all signing one hash (a round's votes: Vote has no voter
+                     field, consensus.rs:169-175): one ovh_verify_batch (host buffers, same-message
+                     path: one hash_to_G2 + one Miller loop for the batch), median of 3
+      round99_ms     the ingress shim (ingress.VoteIngress at proc_network_msg) on a relayer of a
+                     100-validator round: 99 SignedVote messages in, decode + device vote digests
+                     + one same-message prefetch, the N-1 trigger flushing them to overlord;
+                     median of 3 rounds"""
     import torch
     from consensus_overlord_amd import device as dev
     lib = ctx.lib
@@ -244,7 +255,114 @@ def latencies(ctx, sigs, hs, pks) -> dict:
     out["cfg5_ms"] = med(lambda: cfg5(d5), 3)
     out["cfg5_valid_ms"] = med(lambda: cfg5(sigs[:m]), 3)
     out["cfg5_verifs_per_s"] = round(m / (out["cfg5_ms"] * 1e-3), 1)
+    out.update(samemsg_probes(ctx, pks))
     return out
+
+
+def samemsg_probes(ctx, pks) -> dict:
+    """Same-message batches: the config-3 keys signing one hash through
+    ovh_verify_batch, and one 100-validator round through the ingress shim (latencies doc)."""
+    import torch
+    from consensus_overlord_amd import device as dev
+    from consensus_overlord_amd import ingress as ig
+    from consensus_overlord_amd.crypto import FLAG_SK_RAW, ConsensusCrypto, Context
+    from consensus_overlord_amd.vote import PRECOMMIT, rlp_vote
+    lib = ctx.lib
+    out = {}
+    n = pks.shape[0]
+    buf = ctypes.create_string_buffer(32)
+    msg = rlp_vote(7, 0, PRECOMMIT, hashlib.sha256(b"samemsg block").digest())
+    assert lib.ovh_sm3(msg, len(msg), buf) == 0
+    digest = buf.raw
+    sks_h, _ = synth_inputs(lib, 0, n)
+    sks = torch.from_numpy(sks_h).cuda()
+    hs1 = torch.from_numpy(np.tile(np.frombuffer(digest, dtype=np.uint8), (n, 1))).cuda()
+    sg = dev.sign_batch(ctx, sks, hs1).cpu().numpy()
+    pk = pks.cpu().numpy()
+    codes = np.zeros(n, dtype=np.int32)
+    st0 = (ctypes.c_uint64 * 3)()
+    assert lib.ovh_samemsg_stats(ctx.ptr, st0) == 0
+
+    def run():
+        assert lib.ovh_verify_batch(ctx.ptr, n, sg.tobytes(), digest * n, pk.tobytes(),
+                                    codes.ctypes.data_as(ctypes.c_void_p)) == 0
+    run()
+    st1 = (ctypes.c_uint64 * 3)()
+    assert lib.ovh_samemsg_stats(ctx.ptr, st1) == 0
+    if (codes != 0).any() or st1[0] - st0[0] != 1:
+        raise RuntimeError("same-message batch: rejected votes or the path was not taken")
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        run()
+        ts.append(time.perf_counter() - t)
+    out["samemsg4096_ms"] = round(float(np.median(ts)) * 1e3, 3)
+    out["samemsg4096_verifs_per_s"] = round(n / float(np.median(ts)), 1)
+    # ingress: validator 0 is this node; validators 1..99 send their precommits
+    nv = 100
+    vs = torch.from_numpy(sks_h[:nv].copy()).cuda()
+    vpk = dev.sk_to_pk_batch(ctx, vs).cpu().numpy()
+    node = ConsensusCrypto(bytes(sks_h[0]), ctx=Context(torch.cuda.current_device(), flags=FLAG_SK_RAW))
+    node.update_pubkeys([bytes(x) for x in vpk])
+    rts = []
+    for rnd in range(4):
+        msg = rlp_vote(8, rnd, PRECOMMIT, hashlib.sha256(b"round block").digest())
+        assert lib.ovh_sm3(msg, len(msg), buf) == 0
+        d = buf.raw
+        rs = dev.sign_batch(ctx, vs, torch.from_numpy(np.tile(np.frombuffer(d, dtype=np.uint8), (nv, 1))).cuda())
+        rs = rs.cpu().numpy()
+        wire = [ig.encode_signed_vote(ig.SignedVote(bytes(rs[i]), 8, rnd, PRECOMMIT,
+                                                    hashlib.sha256(b"round block").digest(), bytes(vpk[i])))
+                for i in range(1, nv)]
+        fwd = []
+        sh = ig.VoteIngress(node, lambda k, m: fwd.append(m), max_delay_s=1e9)
+        t = time.perf_counter()
+        for w in wire:
+            sh.proc_network_msg(ig.SIGNED_VOTE, w)
+        dt = time.perf_counter() - t
+        if len(fwd) != nv - 1 or sh.stats["batches"] != 1:
+            raise RuntimeError("ingress round: %d forwarded, %d batches" % (len(fwd), sh.stats["batches"]))
+        for m in fwd[:3]:
+            ig.overlord_verify(node, ig.SIGNED_VOTE, m)
+        if rnd:
+            rts.append(dt)
+    out["round99_ms"] = round(float(np.median(rts)) * 1e3, 3)
+    node.ctx.close()
+    return out
+
+
+def vote_clock(sigs, hs, pks, seconds: float):
+    """The clock the vote kernel holds under load (MI355X_MICROARCH.md, DVFS give-back): a
+    context with OVH_FLAG_VM_CLOCK runs pipelined batches back to back for `seconds`, then every
+    workgroup of the last vote launch reports delta s_memtime / delta s_memrealtime around its
+    program (ovh_vm_clock). Untimed diagnostic pass after the measured region; no stamp runs in
+    the measured context."""
+    import torch
+    from consensus_overlord_amd import device as dev
+    from consensus_overlord_amd.crypto import Context
+    c = Context(torch.cuda.current_device(), flags=OVH_FLAG_VM_CLOCK)
+    out = torch.empty((4, sigs.shape[0]), dtype=torch.int32, device="cuda")
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(8):
+            dev.verify_batch_async(c, sigs, hs, pks, out[k % 4])
+            k += 1
+        dev.batch_wait(c)
+    n = c.lib.ovh_vm_clock(c.ptr, None, 0)
+    buf = (ctypes.c_uint64 * max(1, n))()
+    assert c.lib.ovh_vm_clock(c.ptr, buf, n) == n
+    st = np.frombuffer(buf, dtype=np.uint64)[:n].reshape(-1, 2).astype(np.float64)
+    st = st[st[:, 1] > 0]
+    ghz = np.sort(st[:, 0] / st[:, 1] * 0.1)
+    c.close()
+    if not len(ghz):
+        return None
+    return {"clock_ghz": round(float(np.median(ghz)), 3),
+            "p10_p90_ghz": [round(float(ghz[len(ghz) // 10]), 3), round(float(ghz[len(ghz) * 9 // 10]), 3)],
+            "workgroups": int(len(ghz)), "batches": k, "seconds": round(time.perf_counter() - t0, 2),
+            "basis": "median over the last vote launch's workgroups of delta s_memtime / delta s_memrealtime "
+                     "x 100 MHz after back-to-back batches (OVH_FLAG_VM_CLOCK diagnostic context)"}
 
 
 def multi_device_leg(args) -> None:
@@ -302,6 +420,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="skip the untimed latency probes")
+    ap.add_argument("--clock-seconds", type=float, default=2.0,
+                    help="diagnostic pass after the timed region: back-to-back batches on a context with "
+                         "OVH_FLAG_VM_CLOCK for this long, then the vote kernel's held clock (0 = skip)")
     ap.add_argument("--shard-path", action="store_true",
                     help="diagnostic: run the multi-GPU pipeline (partials + RCCL all-gather) even at N=1")
     ap.add_argument("--multi-device", default=None, metavar="DEVS",
@@ -405,6 +526,7 @@ def main():
     bad = int((codes != 0).sum().item())
     if bad:
         raise RuntimeError("batch verify rejected %d valid votes" % bad)
+    clock = vote_clock(sigs, hs, pks, args.clock_seconds) if (rank == 0 and args.clock_seconds > 0) else None
 
     if rank == 0:
         with open(os.path.join(ROOT, "consensus_overlord_amd", "workmodel.json")) as fh:
@@ -436,6 +558,7 @@ def main():
         prog_achieved = Mu[STAGE_TO_WORK[dname]] * units * macs_per_M / (avg_ms[dom] * 1e-3) / 1e12
         value = world * B * args.steps / elapsed
         path_M = W_V_CANON
+        held = clock["clock_ghz"] if clock else None
         line = {
             "metric": "BLS12-381 vote verifications/sec (batch 4096) at 1/2/4/8 MI355X vs host blst",
             "value": round(value, 2),
@@ -460,7 +583,16 @@ def main():
                 "peak": round(PEAK_MAD_U64 / 1e12, 3),
                 "unit": "TOP/s (32x32-bit integer MAC lane-ops; peak = measured v_mad_u64_u32 rate)",
                 "frac": round(achieved * 1e12 / PEAK_MAD_U64, 4),
+                "peak_basis": "v_mad_u64_u32 lane-op rate measured by tools/ubench/int_rates.hip at its best "
+                              "occupancy (profiles/r04_int_rates.json), at the clock that run held (%s GHz)"
+                              % (PEAK_MAD_U64_CLOCK_GHZ,),
+                "peak_fullrate": round(PEAK_FULLRATE / 1e12, 3),
                 "frac_of_fullrate_valu": round(achieved * 1e12 / PEAK_FULLRATE, 4),
+                "fullrate_basis": "SURVEY 8(d): 256 CU x 64 lanes/clk x 2.4 GHz (one wave instruction per 4 "
+                                  "cycles per SIMD)",
+                "vote_clock": clock,
+                "frac_of_fullrate_at_held_clock": (round(achieved * 1e12 / (256 * 64 * held * 1e9), 4)
+                                                   if held else None),
                 "work_M_per_unit": work_M,
                 "work_basis": "SURVEY 8(d) canonical W_v minus MSM + merge + amortised FE" if dname in canon
                               else "program heavy ops (workmodel.json)",

@@ -38,6 +38,7 @@ SIGNATURES = [
     ("ovh_cache_config", ctypes.c_int, [_vp, _sz]),
     ("ovh_cache_stats", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
     ("ovh_msg_cache_stats", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
+    ("ovh_samemsg_stats", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64)]),
     ("ovh_verify_qc_batch", ctypes.c_int, [_vp, _sz, _u8p, _u8p, _u8p, _sz, _vp]),
     ("ovh_set_test_rlc", ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64]),
     ("ovh_verify_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp]),
@@ -51,6 +52,7 @@ SIGNATURES = [
     ("ovh_stage_times", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_float), _sz]),
     ("ovh_stage_name", ctypes.c_char_p, [ctypes.c_int]),
     ("ovh_vm_trace", ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), _sz]),
+    ("ovh_vm_clock", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), _sz]),
     ("ovh_sign_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp]),
     ("ovh_sk_to_pk_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp]),
 ]

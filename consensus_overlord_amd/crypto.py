@@ -282,6 +282,12 @@ class ConsensusCrypto:
         raise_for(self.lib.ovh_cache_stats(self.ctx.ptr, st))
         return tuple(int(x) for x in st)
 
+    def samemsg_stats(self):
+        """(batches, votes, distinct hashes) checked by the same-message path (ovh_samemsg_stats)."""
+        st = (ctypes.c_uint64 * 3)()
+        raise_for(self.lib.ovh_samemsg_stats(self.ctx.ptr, st))
+        return tuple(int(x) for x in st)
+
     def verify_qc_batch(self, signatures, hashes, bitmaps) -> np.ndarray:
         """Batched QC check (ovh_verify_qc_batch): QC j signed by the validators (update_pubkeys)
         selected by bitmaps[j] over the key-sorted validator list; codes[j] equals

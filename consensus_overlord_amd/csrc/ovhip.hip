@@ -217,6 +217,28 @@ struct VmDev {  // a program in device memory
   const uint16_t* in;   // device copies of the slot maps
   const uint16_t* out;
   uint64_t* trace;  // OVH_FLAG_VM_TRACE: nphases + 1 timestamps of workgroup 0, else null
+  uint64_t* clk;    // OVH_FLAG_VM_CLOCK (vote / vote_t): per workgroup (d memtime, d realtime), else null
+};
+
+// OVH_FLAG_VM_CLOCK: shader-cycle and 100 MHz stamps around a workgroup's program (diagnostic
+// runs of the measurement only; a null pointer executes no stamp). Capacity: VM_CLOCK_WGS
+// workgroups of one launch.
+#define VM_CLOCK_WGS (1u << 16)
+struct ClockStamp {
+  uint64_t t0 = 0, r0 = 0;
+  __device__ __forceinline__ void begin(const uint64_t* clk) {
+    if (clk && threadIdx.x == 0) {
+      t0 = __builtin_amdgcn_s_memtime();
+      r0 = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+  __device__ __forceinline__ void end(uint64_t* clk) {
+    if (clk && threadIdx.x == 0 && blockIdx.x < VM_CLOCK_WGS) {
+      const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+      clk[2 * blockIdx.x] = t1 - t0;
+      clk[2 * blockIdx.x + 1] = r1 - r0;
+    }
+  }
 };
 
 // Batches of at most SMALL_MAX votes (one vote per wave: 1,024 waves fill the chip's SIMDs)
@@ -352,9 +374,12 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
   }
   __syncthreads();
   vote_stagger();
+  ClockStamp cs;
+  cs.begin(prog.clk);
   vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, vote_scalar(seed, base, i),
           vm::Out{s.p, s.cap, i},
           blockIdx.x == 0 ? prog.trace : nullptr);
+  cs.end(prog.clk);
   if (active && lane == 0) {
     const uint32_t pf = hdr[0];
     const uint32_t pk_bad = pf & 1, pk_inf = (pf >> 1) & 1, pk_xz = (pf >> 2) & 1;
@@ -494,8 +519,11 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
   }
   __syncthreads();
   vote_stagger();
+  ClockStamp cs;
+  cs.begin(prog.clk);
   vm::run(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst, vote_scalar(seed, base, i),
           vm::Out{s.p, s.cap, i}, blockIdx.x == 0 ? prog.trace : nullptr);
+  cs.end(prog.clk);
   if (active && lane == 0) {
     const uint32_t sf = hdr[0], pf = hdr[1];
     const uint32_t sg_bad = sf & 1, sg_inf = (sf >> 1) & 1, sg_xz = (sf >> 2) & 1;
@@ -681,6 +709,236 @@ __global__ __launch_bounds__(64) void k_vm_votew(uint32_t n, VmDev prog, const u
   else
     vote_wave<false>(prog, VM_VOTEW_NPHASES, VM_VOTEW_NSLOTS, VM_VOTEW_IN, VM_VOTEW_OUT, cst_g, pks + (size_t)i * 48,
                      pk, e, sigs + (size_t)i * 96, s, i, vote_scalar(seed, base, i), codes + i);
+}
+
+// ------------------------------------------------------------------ same-message batches (r04)
+// A round's votes all sign one hash (consensus.rs:169-175: Vote carries no voter), so a batch of
+// n votes over G distinct hashes is checked as
+//   prod_g e(sum_{i in g} r_i pk_i, H_g) * e(-G1, sum_i r_i sigma_i) == 1
+// (verify_samemsg_locked): one hash_to_G2 (k_vm_h2g) and one Miller loop
+// (k_vm_gmil) per distinct hash; per vote only the key / signature checks and r_i pk_i
+// (k_vm_vsame, programs vsame / vsame_t). Group slab planes (per distinct hash, gcap entries):
+// u0, u1 | H | f (tools/fpvm/progs.py G_U, G_H, G_F).
+constexpr uint32_t VSAME_NSLOTS = VM_VSAME_NSLOTS > VM_VSAME_T_NSLOTS ? VM_VSAME_NSLOTS : VM_VSAME_T_NSLOTS;
+constexpr uint32_t VSAME_STRIDE_W = align256w(VSAME_NSLOTS * 12 + 4);
+constexpr uint32_t H2G_STRIDE_W = align256w(VM_H2G_NSLOTS * 12);
+static_assert(VM_VSAME_W == 16 && VM_VSAME_T_W == 16 && VM_H2G_W == 16 && VM_GMIL_W == 64 && VM_H2G_NIN == 4 &&
+                  VM_GMIL_NIN == 9 && VM_G_U == 0 && VM_G_PLANES == 22,
+              "same-message program shapes (tools/fpvm/progs.py)");
+
+// Per vote (16-lane slice, 4 per workgroup): votes lo + j, j < cnt (key bytes at pks + 48 j, or
+// table entry pk.idx[j]; signature at sigs + 96 j); stores sigma, tau and r pk at slab index
+// lo + j; code in the reference precedence without the H = O case (k_samemsg_fix adds it).
+template <bool TABLE>
+__global__ __launch_bounds__(64) void k_vm_vsame(uint32_t cnt, uint32_t lo, VmDev prog,
+                                                 const uint32_t* __restrict__ cst_g, const uint8_t* __restrict__ pks,
+                                                 PkSrc pk, const uint8_t* __restrict__ sigs, Slab s, uint64_t seed,
+                                                 uint64_t base, int32_t* __restrict__ codes) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / 16, lane = threadIdx.x % 16;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * VSAME_STRIDE_W;
+  constexpr uint32_t NS = TABLE ? VM_VSAME_T_NSLOTS : VM_VSAME_NSLOTS;
+  uint32_t* hdr = slots + NS * 12;  // [sig flags, key flags]
+  const uint16_t* IN = TABLE ? VM_VSAME_T_IN : VM_VSAME_IN;
+  const uint32_t j = blockIdx.x * VM_SLICES + slice, i = lo + j;
+  const bool active = j < cnt;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active) {
+    if (lane == 0) {
+      uint32_t x1[12], x0[12], bad, inf, sort, xz;
+      parse_hdr(sigs + (size_t)j * 96, 96, x1, x0, bad, inf, sort, xz);
+      slot_put(slots, IN[TABLE ? VM_VSAME_T_IN_SIG_X1 : VM_VSAME_IN_SIG_X1], x1);
+      slot_put(slots, IN[TABLE ? VM_VSAME_T_IN_SIG_X0 : VM_VSAME_IN_SIG_X0], x0);
+      slot_flag(slots, IN[TABLE ? VM_VSAME_T_IN_SIG_SORT : VM_VSAME_IN_SIG_SORT], sort);
+      hdr[0] = bad | inf << 1 | xz << 2;
+    } else if (lane == 1) {
+      if constexpr (TABLE) {
+        hdr[1] = pk.flags[pk.idx[j]];
+      } else {
+        uint32_t x[12], bad, inf, sort, xz;
+        parse_hdr(pks + (size_t)j * 48, 48, x, x, bad, inf, sort, xz);
+        slot_put(slots, IN[VM_VSAME_IN_PK_X], x);
+        slot_flag(slots, IN[VM_VSAME_IN_PK_SORT], sort);
+        hdr[1] = bad | inf << 1 | xz << 2;
+      }
+    } else if (TABLE && lane >= 2 && lane < 5) {
+      Fp v;
+      Slab{const_cast<uint32_t*>(pk.planes), pk.cap}.ld(v, lane - 2, (uint32_t)pk.idx[j]);
+      slot_put(slots, IN[VM_VSAME_T_IN_PK_X + (lane - 2)], v.v);
+    }
+  }
+  __syncthreads();
+  vm::run(prog.code, TABLE ? VM_VSAME_T_NPHASES : VM_VSAME_NPHASES, 16, lane, active, slots, cst,
+          vote_scalar(seed, base, i), vm::Out{s.p, s.cap, i});
+  if (active && lane == 0) {
+    const uint32_t sf = hdr[0], pf = hdr[1];
+    const uint32_t sg_bad = sf & 1, sg_inf = (sf >> 1) & 1, sg_xz = (sf >> 2) & 1;
+    uint32_t kf = pf, sg_ok, sg_grp;
+    if constexpr (TABLE) {
+      sg_ok = slot_flag_get(slots, VM_VSAME_T_OUT[VM_VSAME_T_OUT_SIG_OK]);
+      sg_grp = slot_flag_get(slots, VM_VSAME_T_OUT[VM_VSAME_T_OUT_SIG_GRP]);
+    } else {
+      sg_ok = slot_flag_get(slots, VM_VSAME_OUT[VM_VSAME_OUT_SIG_OK]);
+      sg_grp = slot_flag_get(slots, VM_VSAME_OUT[VM_VSAME_OUT_SIG_GRP]);
+      const uint32_t pk_ok = slot_flag_get(slots, VM_VSAME_OUT[VM_VSAME_OUT_PK_OK]);
+      const uint32_t pk_grp = slot_flag_get(slots, VM_VSAME_OUT[VM_VSAME_OUT_PK_GRP]);
+      const uint32_t pk_bad = pf & 1, pk_inf = (pf >> 1) & 1, pk_xz = (pf >> 2) & 1;
+      kf = (pk_bad || (!pk_inf && (!pk_ok || pk_xz))) ? PKF_PARSE : pk_inf ? PKF_INF : !pk_grp ? PKF_GRP : 0u;
+    }
+    int32_t c;  // consensus.rs:397-416, as k_vm_vote; H(m) = O is added per group (k_samemsg_fix)
+    if (kf & PKF_PARSE) c = OVH_ERR_PUBKEY;
+    else if (sg_bad) c = BLST_BAD_ENCODING;
+    else if (!sg_inf && !sg_ok) c = BLST_POINT_NOT_ON_CURVE;
+    else if (!sg_inf && (sg_xz || !sg_grp)) c = BLST_POINT_NOT_IN_GROUP;
+    else if (kf & PKF_INF) c = BLST_PK_IS_INFINITY;
+    else if (kf & PKF_GRP) c = BLST_POINT_NOT_IN_GROUP;
+    else if (sg_inf) c = BLST_VERIFY_FAIL;
+    else c = 0;
+    codes[i] = c;
+  }
+}
+
+// hash_to_G2 per distinct hash (16-lane slice, 4 per workgroup): u planes of group g -> H planes
+// of group g, ghinf[g] = H is the identity.
+__global__ __launch_bounds__(64) void k_vm_h2g(uint32_t G, VmDev prog, const uint32_t* __restrict__ cst_g, Slab g,
+                                               uint32_t* __restrict__ ghinf) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / 16, lane = threadIdx.x % 16;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * H2G_STRIDE_W;
+  const uint32_t q = blockIdx.x * VM_SLICES + slice;
+  const bool active = q < G;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active && lane < 4) {
+    Fp u;
+    g.ld(u, VM_G_U + lane, q);
+    slot_put(slots, VM_H2G_IN[lane], u.v);
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_H2G_NPHASES, 16, lane, active, slots, cst, 0, vm::Out{g.p, g.cap, q});
+  if (active && lane == 0) ghinf[q] = slot_flag_get(slots, VM_H2G_OUT[VM_H2G_OUT_H_INF]) ? 1u : 0u;
+}
+
+// Lane per vote: a vote whose hash maps to the identity (H_g = O) fails with VERIFY_FAIL when
+// nothing earlier failed (k_vm_vote's precedence); every vote with a non-zero code contributes
+// the identity to its group's key sum (r pk := (0 : 1 : 0)).
+__global__ __launch_bounds__(WG) void k_samemsg_fix(uint32_t n, const uint32_t* __restrict__ gid,
+                                                    const uint32_t* __restrict__ ghinf, int32_t* __restrict__ codes,
+                                                    Slab P) {
+  const uint32_t i = blockIdx.x * WG + threadIdx.x;
+  if (i >= n) return;
+  int32_t c = codes[i];
+  if (c == 0 && ghinf[gid[i]]) codes[i] = c = BLST_VERIFY_FAIL;
+  if (c != 0) {
+    Fp z, o;
+    fp_zero(z);
+    fp_one(o);
+    P.st(z, 0, i);
+    P.st(o, 1, i);
+    P.st(z, 2, i);
+  }
+}
+
+// One level of the per-hash key sums: pair k = (a, b) -> P[a] = P[a] + P[b] (g1padd, complete
+// formulas), one pair per 8-lane slice. The host plans the levels (samemsg_plan): the pairs of a
+// level are disjoint, so the update is in place.
+__global__ __launch_bounds__(64) void k_vm_g1pairs(uint32_t npairs, VmDev prog, uint32_t stride_w,
+                                                   const uint32_t* __restrict__ cst_g, const uint32_t* __restrict__ pairs,
+                                                   Slab P) {
+  constexpr uint32_t W = VM_G1PADD_W, SL = 64 / W;
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / W, lane = threadIdx.x % W;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * stride_w;
+  const uint32_t q = blockIdx.x * SL + slice;
+  const bool active = q < npairs;
+  const uint32_t a = active ? pairs[2 * q] : 0u, b = active ? pairs[2 * q + 1] : 0u;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active) {
+    for (uint32_t k = lane; k < 6; k += W) {
+      Fp v;
+      P.ld(v, k % 3, k < 3 ? a : b);
+      slot_put(slots, prog.in[k], v.v);
+    }
+  }
+  __syncthreads();
+  vm::run(prog.code, prog.nphases, W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  if (active) {
+    for (uint32_t k = lane; k < 3; k += W) {
+      Fp v;
+      const uint32_t src = prog.out[k];
+      for (int l = 0; l < 12; ++l) v.v[l] = slots[src * 12 + l];
+      vm::canon(v, v);
+      P.st(v, k, a);
+    }
+  }
+}
+
+// Per distinct hash (one wave): f_g = Miller(apk_g, H_g) -> the group slab's f planes; apk_g =
+// P[head[g]] (its votes' r pk summed, the identity when none of them passed its checks or
+// H_g = O), and then f_g = 1 (e(O, H) = 1).
+__global__ __launch_bounds__(64) void k_vm_gmil(uint32_t G, VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                const uint32_t* __restrict__ head, Slab P, Slab g) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  uint32_t* slots = lds + SLOT_BASE_W;
+  __shared__ uint32_t zinf;
+  const uint32_t q = blockIdx.x, lane = threadIdx.x;
+  if (q >= G) return;
+  const uint32_t a = head[q];
+  load_consts(cst, cst_g, VM_NCONST);
+  if (lane == 0) {
+    Fp z;
+    P.ld(z, 2, a);
+    zinf = fp_is_zero(z) ? 1u : 0u;
+  }
+  if (lane < 9) {
+    Fp v;
+    if (lane < 3) P.ld(v, lane, a);
+    else g.ld(v, VM_G_H + (lane - 3), q);
+    slot_put(slots, VM_GMIL_IN[lane], v.v);
+  }
+  __syncthreads();
+  if (zinf) {  // wave-uniform
+    if (lane < 12) {
+      Fp v;
+      if (lane == 0) fp_one(v);
+      else fp_zero(v);
+      g.st(v, VM_G_F + lane, q);
+    }
+    return;
+  }
+  vm::run(prog.code, VM_GMIL_NPHASES, 64, lane, true, slots, cst, 0, vm::Out{g.p, g.cap, q});
+}
+
+// The bisection of a same-message batch whose combined check failed (skipped when *verdict == 1):
+// every vote with code 0 of [lo, lo + cnt) on a whole wave, vote1h / vote_t1h with its hash's H
+// -> f_i = Miller(pk, H) Miller(-G1, sigma) in the slab's f planes; k_vm_votefe then checks
+// FE(f_i) == 1 per vote.
+template <bool TABLE>
+__global__ __launch_bounds__(64) void k_vm_vote1h_b(uint32_t cnt, uint32_t lo, VmDev prog,
+                                                    const uint32_t* __restrict__ cst_g,
+                                                    const uint8_t* __restrict__ pks, PkSrc pk,
+                                                    const uint8_t* __restrict__ sigs, Slab s, int32_t* __restrict__ codes,
+                                                    const uint32_t* __restrict__ gid, Slab gH,
+                                                    const uint32_t* __restrict__ ghinf,
+                                                    const int32_t* __restrict__ verdict) {
+  if (*verdict == 1) return;
+  const uint32_t j = blockIdx.x, i = lo + j;
+  if (j >= cnt || codes[i] != 0) return;
+  const uint32_t e = TABLE ? (uint32_t)pk.idx[j] : 0u;
+  if constexpr (TABLE)
+    vote_wave<true, true>(prog, VM_VOTE_T1H_NPHASES, VM_VOTE_T1H_NSLOTS, VM_VOTE_T1H_IN, VM_VOTE_T1H_OUT, cst_g,
+                          nullptr, pk, e, sigs + (size_t)j * 96, s, i, 1, codes + i, gH, gid[i], ghinf + gid[i]);
+  else
+    vote_wave<false, true>(prog, VM_VOTE1H_NPHASES, VM_VOTE1H_NSLOTS, VM_VOTE1H_IN, VM_VOTE1H_OUT, cst_g,
+                           pks + (size_t)j * 48, pk, e, sigs + (size_t)j * 96, s, i, 1, codes + i, gH, gid[i],
+                           ghinf + gid[i]);
 }
 
 // verify_aggregated_signature (verify_aggregated_vm), the part without the aggregated key, on a
@@ -1658,6 +1916,13 @@ struct ovh_ctx {
   std::deque<HostBatch> hq;  // batches in flight (the root context / a single context)
   uint64_t hb_k = 0;
   // Fp-VM programs + constant table in device memory
+  // same-message batches (verify_samemsg_locked): programs, per slot the group slab (G_PLANES
+  // planes + the H-is-infinity words, gcap entries); OVH_SAMEMSG=0 turns the path off
+  VmDev vm_vsame{}, vm_vsame_t{}, vm_h2g{}, vm_gmil{};
+  uint32_t* gslab[OVH_BATCH_SLOTS] = {};
+  uint32_t gcap[OVH_BATCH_SLOTS] = {};
+  bool samemsg = true;
+  uint64_t sm_batches = 0, sm_votes = 0, sm_hashes = 0;
   VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{},
       vm_pkchk{}, vm_g1padd{}, vm_vote1{}, vm_vote_t1{}, vm_final1{}, vm_votew{},
       vm_votew_t{}, vm_qcpre{}, vm_qcmil{}, vm_vote1h{}, vm_vote_t1h{}, vm_pkgen{}, vm_signg0{}, vm_signg1{};
@@ -1671,6 +1936,8 @@ struct ovh_ctx {
   uint64_t hc_hits = 0, hc_misses = 0;
   uint32_t* vm_consts = nullptr;
   std::vector<void*> vm_bufs;
+  uint32_t clk_wgs = 0;    // OVH_FLAG_VM_CLOCK: workgroups of the last vote launch
+  bool clk_table = false;  // ... and whether it was vote_t
   std::vector<uint32_t> blind_h;  // host copy of the last compression blinds (upload_blinds)
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
   hipEvent_t ev0[OVH_NSTAGES] = {}, ev1[OVH_NSTAGES] = {};
@@ -1730,6 +1997,10 @@ static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1
                   LDS_QCMIL <= 64 * 1024 && VM_G1PADD_NIN == 6,
               "default LDS limit");
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
+static constexpr size_t LDS_VSAME = ((size_t)SLOT_BASE_W + VM_SLICES * (size_t)VSAME_STRIDE_W) * 4;
+static constexpr size_t LDS_H2G = ((size_t)SLOT_BASE_W + VM_SLICES * (size_t)H2G_STRIDE_W) * 4;
+static constexpr size_t LDS_GMIL = ((size_t)SLOT_BASE_W + (size_t)VM_GMIL_NSLOTS * 12) * 4;
+static_assert(LDS_VSAME <= 64 * 1024 && LDS_H2G <= 64 * 1024 && LDS_GMIL + 16 <= 64 * 1024, "same-message LDS");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
 // allocation granules assumed)
 constexpr size_t lds_granule(size_t b) { return (b + 1023) / 1024 * 1024; }
@@ -1758,6 +2029,14 @@ static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphase
   d.in = (const uint16_t*)di;
   d.out = (const uint16_t*)dout;
   d.trace = nullptr;
+  d.clk = nullptr;
+  if ((c->flags & OVH_FLAG_VM_CLOCK) && (code == VM_VOTE_CODE || code == VM_VOTE_T_CODE)) {
+    void* dk = nullptr;
+    HIPCHK(hipMalloc(&dk, (size_t)2 * VM_CLOCK_WGS * 8));
+    c->vm_bufs.push_back(dk);
+    HIPCHK(hipMemset(dk, 0, (size_t)2 * VM_CLOCK_WGS * 8));
+    d.clk = (uint64_t*)dk;
+  }
   if (c->flags & OVH_FLAG_VM_TRACE) {
     void* dt = nullptr;
     HIPCHK(hipMalloc(&dt, ((size_t)nphases + 1) * 8));
@@ -1808,6 +2087,13 @@ static int vm_init(ovh_ctx* c) {
                 VM_VOTEW_T_NIN, VM_VOTEW_T_OUT, VM_VOTEW_T_NOUT));
   CHK(vm_upload(c, c->vm_final1, VM_FINAL1_CODE, VM_FINAL1_NPHASES, VM_FINAL1_W, VM_FINAL1_NW, VM_FINAL1_IN,
                 VM_FINAL1_NIN, VM_FINAL1_OUT, VM_FINAL1_NOUT));
+  CHK(vm_upload(c, c->vm_vsame, VM_VSAME_CODE, VM_VSAME_NPHASES, VM_VSAME_W, VM_VSAME_NW, VM_VSAME_IN, VM_VSAME_NIN,
+                VM_VSAME_OUT, VM_VSAME_NOUT));
+  CHK(vm_upload(c, c->vm_vsame_t, VM_VSAME_T_CODE, VM_VSAME_T_NPHASES, VM_VSAME_T_W, VM_VSAME_T_NW, VM_VSAME_T_IN,
+                VM_VSAME_T_NIN, VM_VSAME_T_OUT, VM_VSAME_T_NOUT));
+  CHK(vm_upload(c, c->vm_h2g, VM_H2G_CODE, VM_H2G_NPHASES, VM_H2G_W, VM_H2G_NW, VM_H2G_IN, VM_H2G_NIN, VM_H2G_OUT,
+                VM_H2G_NOUT));
+  CHK(vm_upload(c, c->vm_gmil, VM_GMIL_CODE, VM_GMIL_NPHASES, VM_GMIL_W, VM_GMIL_NW, VM_GMIL_IN, VM_GMIL_NIN, nullptr, 0));
   CHK(vm_upload(c, c->vm_g1padd, VM_G1PADD_CODE, VM_G1PADD_NPHASES, VM_G1PADD_W, VM_G1PADD_NW, VM_G1PADD_IN,
                 VM_G1PADD_NIN, VM_G1PADD_OUT, VM_G1PADD_NOUT));
   CHK(vm_upload(c, c->vm_madd, VM_MADD_CODE, VM_MADD_NPHASES, VM_MADD_W, VM_MADD_NW, VM_MADD_IN, VM_MADD_NIN, VM_MADD_OUT,
@@ -2035,6 +2321,8 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
       k_vm_vote_t<<<nwg, 64, LDS_VOTE_T, st>>>(n, c->vm_vote_t, c->vm_fold, c->vm_consts, key.pts, d_sigs, s, seed,
                                                base, d_codes, region_F(c, slot, 0), c->vstart);
     c->vlaunched += nwg;
+    c->clk_wgs = nwg < VM_CLOCK_WGS ? nwg : VM_CLOCK_WGS;
+    c->clk_table = key.bytes == nullptr;
   }
   if (fold1) {  // fold level 1: R0 -> R1 (one partial per 16-vote group)
     StageScope p(c, ST_FOLD);
@@ -2419,18 +2707,182 @@ static KeySrc staged_key(ovh_ctx* c, size_t n, uint8_t* d, size_t t, size_t lo) 
   return KeySrc{d + n * 128 + 48 * lo, PkSrc{}};
 }
 
+// ---- same-message batches
+// Host plan of a staged batch: the distinct hashes (in first-seen order), each vote's group, the
+// per-group pairwise-sum levels of its votes' r pk (pairs (a, b): P[a] += P[b], disjoint within a
+// level) and each group's root. Device layout at offset `off` of the staging buffer:
+// gid (4 n) | distinct hashes (32 G) | heads (4 G) | pairs (8 per pair, level by level).
+struct SameMsgPlan {
+  uint32_t G = 0;
+  std::vector<uint32_t> gid, head, pairs, level_off;  // level_off: pair offsets, one past the last
+  std::vector<uint8_t> ghash;
+  size_t off = 0, bytes = 0;
+};
+
+static void samemsg_plan(size_t n, const uint8_t* hashes, const std::vector<uint32_t>& perm, SameMsgPlan& pl) {
+  std::unordered_map<std::string, uint32_t> idx;
+  std::vector<std::vector<uint32_t>> members;
+  pl.gid.resize(n);
+  std::string k(32, '\0');
+  for (size_t j = 0; j < n; ++j) {
+    const size_t i = perm.empty() ? j : perm[j];
+    memcpy(&k[0], hashes + 32 * i, 32);
+    auto it = idx.find(k);
+    uint32_t g;
+    if (it == idx.end()) {
+      g = (uint32_t)members.size();
+      idx.emplace(k, g);
+      members.emplace_back();
+      pl.ghash.insert(pl.ghash.end(), hashes + 32 * i, hashes + 32 * i + 32);
+    } else {
+      g = it->second;
+    }
+    pl.gid[j] = g;
+    members[g].push_back((uint32_t)j);
+  }
+  pl.G = (uint32_t)members.size();
+  for (const auto& m : members) pl.head.push_back(m[0]);
+  pl.level_off.push_back(0);
+  for (size_t stride = 1;; stride <<= 1) {
+    bool any = false;
+    for (const auto& m : members)
+      for (size_t q = 0; q + stride < m.size(); q += 2 * stride) {
+        pl.pairs.push_back(m[q]);
+        pl.pairs.push_back(m[q + stride]);
+        any = true;
+      }
+    if (!any) break;
+    pl.level_off.push_back((uint32_t)(pl.pairs.size() / 2));
+  }
+  pl.bytes = 4 * n + 32 * (size_t)pl.G + 4 * (size_t)pl.G + 4 * pl.pairs.size();
+}
+
+// The batch's state is staged at d (stage_split layout: sigs | hashes | pks | codes | table
+// indices; table votes [0, t)); the plan's arrays at d + pl.off. Main stream: the per-vote
+// programs (vsame_t over the table votes, vsame over the others); the slot's final stream, beside
+// them: hash_to_field + hash_to_G2 per distinct hash; then (final stream) the H = O codes, the
+// per-hash sums of r pk, the per-hash Miller loops, their fold, the MSM of sum r_i sigma_i, the
+// final check, and -- gated on its verdict -- the per-vote bisection. Caller holds c->mu.
+static int verify_samemsg_locked(ovh_ctx* c, size_t n, uint8_t* d, size_t t, const SameMsgPlan& pl, int32_t* dc) {
+  CHK(ensure_cap(c, n));
+  int slot;
+  CHK(take_slot(c, &slot));
+  if (!c->gslab[slot] || c->gcap[slot] < c->cap) {
+    if (c->gslab[slot]) (void)hipFree(c->gslab[slot]);
+    c->gslab[slot] = nullptr;
+    HIPCHK(hipMalloc(&c->gslab[slot], ((size_t)VM_G_PLANES * 12 + 1) * c->cap * 4));
+    c->gcap[slot] = c->cap;
+  }
+  const uint32_t G = pl.G, N = (uint32_t)n, T = (uint32_t)t;
+  const Slab g{c->gslab[slot], c->gcap[slot]};
+  uint32_t* ghinf = c->gslab[slot] + (size_t)VM_G_PLANES * 12 * g.cap;
+  const Slab gH{g.p + (size_t)VM_G_H * 12 * g.cap, g.cap};
+  const Slab s{c->state_slot[slot], c->cap};
+  const Slab P{s.p + (size_t)S_F * 12 * s.cap, s.cap};  // r pk of every vote, then the sums in place
+  const uint8_t* ex = d + pl.off;
+  const uint32_t* gid = (const uint32_t*)ex;
+  const uint8_t* ghash = ex + 4 * n;
+  const uint32_t* head = (const uint32_t*)(ghash + 32 * (size_t)G);
+  const uint32_t* pairs = head + G;
+  c->ev_mask = 0;
+  uint64_t seed, base;
+  CHK(draw_seed(c, &seed, &base));
+  c->slot_seed[slot] = seed;
+  c->slot_base[slot] = base;
+  const hipStream_t st = c->stream, fst = c->fs[slot];
+  HIPCHK(hipEventRecord(c->ev_front[slot], st));  // the staged inputs
+  HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
+  {
+    StageScope p(c, ST_H2F, fst);
+    k_h2f<<<nblk(G), WG, 0, fst>>>(G, ghash, c->xmd, g);
+    k_vm_h2g<<<(G + VM_SLICES - 1) / VM_SLICES, 64, LDS_H2G, fst>>>(G, c->vm_h2g, c->vm_consts, g, ghinf);
+  }
+  {
+    StageScope p(c, ST_VOTE, st);
+    const PkSrc tab{c->tab.planes, c->tab.cap, c->tab.flags, (int32_t*)(d + n * 180)};
+    if (T)
+      k_vm_vsame<true><<<(T + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(T, 0, c->vm_vsame_t, c->vm_consts, nullptr,
+                                                                              tab, d, s, seed, base, dc);
+    if (N > T)
+      k_vm_vsame<false><<<(N - T + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(
+          N - T, T, c->vm_vsame, c->vm_consts, d + n * 128 + 48 * (size_t)T, PkSrc{}, d + 96 * (size_t)T, s, seed, base,
+          dc);
+  }
+  HIPCHK(hipEventRecord(c->ev_front[slot], st));
+  HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
+  int reg = 0;
+  uint32_t m = (G + 3) / 4;
+  {
+    StageScope p(c, ST_FOLD, fst);
+    k_samemsg_fix<<<nblk(n), WG, 0, fst>>>(N, gid, ghinf, dc, P);
+    for (size_t l = 0; l + 1 < pl.level_off.size(); ++l) {
+      const uint32_t a = pl.level_off[l], np = pl.level_off[l + 1] - a;
+      k_vm_g1pairs<<<(np + 64 / VM_G1PADD_W - 1) / (64 / VM_G1PADD_W), 64, LDS_G1PADD, fst>>>(
+          np, c->vm_g1padd, G1PADD_STRIDE_W, c->vm_consts, pairs + 2 * (size_t)a, P);
+    }
+    k_vm_gmil<<<G, 64, LDS_GMIL, fst>>>(G, c->vm_gmil, c->vm_consts, head, P, g);
+    k_vm_fold<VM_FOLD_UNITS><<<(m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, fst>>>(
+        G, c->vm_fold, c->vm_consts, Slab{g.p + (size_t)VM_G_F * 12 * g.cap, g.cap}, Slab{nullptr, 0},
+        region_F(c, slot, 0), nullptr);
+  }
+  CHK(fold_down(c, slot, fst, 1, &reg, &m, 4));
+  CHK(enqueue_msm(c, fst, slot, N, dc));
+  int32_t* verdict = c->result + RES_BATCH + slot;
+  enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict, msm_S(c, slot));
+  {
+    StageScope p(c, ST_FALLBACK, fst);
+    const PkSrc tab{c->tab.planes, c->tab.cap, c->tab.flags, (int32_t*)(d + n * 180)};
+    if (T)
+      k_vm_vote1h_b<true><<<T, 64, LDS_VOTE1H, fst>>>(T, 0, c->vm_vote_t1h, c->vm_consts, nullptr, tab, d, s, dc, gid,
+                                                      gH, ghinf, verdict);
+    if (N > T)
+      k_vm_vote1h_b<false><<<N - T, 64, LDS_VOTE1H, fst>>>(N - T, T, c->vm_vote1h, c->vm_consts,
+                                                           d + n * 128 + 48 * (size_t)T, PkSrc{}, d + 96 * (size_t)T, s,
+                                                           dc, gid, gH, ghinf, verdict);
+    k_vm_votefe<<<N, 64, LDS_FINAL1, fst>>>(N, c->vm_final1, c->vm_consts, s, dc, verdict);
+  }
+  HIPCHK(hipEventRecord(c->ev_back[slot], fst));
+  HIPCHK(hipGetLastError());
+  c->slot_n[slot] = N;
+  c->last_n = 0;  // no (f, r sigma) state for ovh_batch_partial_device / the standard bisection
+  ++c->sm_batches;
+  c->sm_votes += n;
+  c->sm_hashes += G;
+  return 0;
+}
+
 // ovh_verify_batch on one device (caller holds c->mu): codes (host) of n votes. Table votes and
 // the others run as two batches (each its own combined check) when a batch mixes them.
 static int verify_host_locked(ovh_ctx* c, size_t n, const uint8_t* sigs, const uint8_t* hashes, const uint8_t* pks,
                               int32_t* codes) {
   HIPCHK(hipSetDevice(c->device));
-  CHK(ensure_in(c, n * (96 + 32 + 48 + 4 + 4) + 64));
+  // same-message batches: at least two votes per distinct hash on average (a round's votes)
+  SameMsgPlan pl;
+  std::vector<uint32_t> perm;
+  std::vector<int32_t> tidx;
+  const size_t t0 = table_split(c, n, pks, perm, tidx);
+  (void)t0;
+  bool same = false;
+  if (c->samemsg && n >= 2) {
+    samemsg_plan(n, hashes, perm, pl);
+    same = 2 * (size_t)pl.G <= n;
+  }
+  pl.off = (n * (96 + 32 + 48 + 4 + 4) + 255) / 256 * 256;
+  CHK(ensure_in(c, same ? pl.off + pl.bytes + 64 : n * (96 + 32 + 48 + 4 + 4) + 64));
   uint8_t* d;
   size_t t;
-  std::vector<uint32_t> perm;
   CHK(stage_split(c, n, sigs, hashes, pks, &d, &t, perm));
   int32_t* dc = (int32_t*)(d + n * 176);
-  if (n == 1) {
+  if (same) {
+    std::vector<uint8_t> h(pl.bytes);
+    memcpy(h.data(), pl.gid.data(), 4 * n);
+    memcpy(h.data() + 4 * n, pl.ghash.data(), 32 * (size_t)pl.G);
+    memcpy(h.data() + 4 * n + 32 * (size_t)pl.G, pl.head.data(), 4 * (size_t)pl.G);
+    if (!pl.pairs.empty()) memcpy(h.data() + 4 * n + 36 * (size_t)pl.G, pl.pairs.data(), 4 * pl.pairs.size());
+    HIPCHK(hipMemcpyAsync(d + pl.off, h.data(), pl.bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));  // the pageable copy of h completed before h dies
+    CHK(verify_samemsg_locked(c, n, d, t, pl, dc));
+  } else if (n == 1) {
     CHK(verify_one_locked(c, d, d + 96, staged_key(c, n, d, t, 0), dc, hashes));
   } else {
     for (int part = 0; part < 2; ++part) {  // table votes [0, t), then the others [t, n)
@@ -2861,6 +3313,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   c->flags = flags;
   if (const char* e = getenv("OVH_FOLD_SIDE")) c->fold_side = atoi(e) != 0;
   if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
+  if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e) != 0;
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->wg_cap = 4u * (uint32_t)ncu;
@@ -2967,7 +3420,8 @@ static void destroy_one(ovh_ctx* c) {
   for (hipStream_t s : {c->fstream, c->fstream2, c->xstream})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
-    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k]})
+    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
+                    (void*)c->gslab[k]})
       if (p) (void)hipFree(p);
   for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vstart, (void*)c->vm_consts,
                   (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
@@ -3016,6 +3470,18 @@ int ovh_vm_trace(ovh_ctx* c, int prog, uint64_t* stamps, size_t max) {
   const size_t n = (size_t)d->nphases + 1, k = max < n ? max : n;
   if (sync_all(c) || (k && hipMemcpy(stamps, d->trace, k * 8, hipMemcpyDeviceToHost) != hipSuccess))
     return -OVH_ERR_DEVICE;
+  return (int)n;
+}
+
+int ovh_vm_clock(ovh_ctx* c, uint64_t* stamps, size_t max) {
+  if (!c || (max && !stamps)) return -OVH_ERR_ARG;
+  if (!c->sub.empty()) c = c->sub[0];
+  if (!(c->flags & OVH_FLAG_VM_CLOCK)) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess || sync_all(c)) return -OVH_ERR_DEVICE;
+  const VmDev* d = c->clk_table ? &c->vm_vote_t : &c->vm_vote;
+  const size_t n = (size_t)2 * c->clk_wgs, k = max < n ? max : n;
+  if (k && hipMemcpy(stamps, d->clk, k * 8, hipMemcpyDeviceToHost) != hipSuccess) return -OVH_ERR_DEVICE;
   return (int)n;
 }
 
@@ -3702,6 +4168,18 @@ int ovh_cache_stats(ovh_ctx* c, uint64_t stats[3]) {
   stats[0] = c->cache.hits;
   stats[1] = c->cache.misses;
   stats[2] = c->cache.map.size();
+  return 0;
+}
+
+int ovh_samemsg_stats(ovh_ctx* c, uint64_t stats[3]) {
+  if (!c || !stats) return OVH_ERR_ARG;
+  stats[0] = stats[1] = stats[2] = 0;
+  for (ovh_ctx* s : devices_of(c)) {
+    std::lock_guard<std::mutex> g(s->mu);
+    stats[0] += s->sm_batches;
+    stats[1] += s->sm_votes;
+    stats[2] += s->sm_hashes;
+  }
   return 0;
 }
 

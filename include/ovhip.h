@@ -50,6 +50,8 @@ typedef struct ovh_ctx ovh_ctx;
 #define OVH_FLAG_TEST_RLC 0x8u          /* TESTS ONLY: batch coefficients from ovh_set_test_rlc (predictable) */
 #define OVH_FLAG_SK_RAW 0x10u           /* private key = 32-byte big-endian scalar 0 < sk < r (blst
                                            SecretKey::from_bytes) instead of KeyGen (see ovh_sk_parse) */
+#define OVH_FLAG_VM_CLOCK 0x20u         /* diagnostics: shader / wall clock stamps around every vote
+                                           workgroup's program (ovh_vm_clock) */
 
 /* Batch stages (ovh_stage_name gives the label). Each stage is one or more kernels. */
 #define OVH_NSTAGES 6
@@ -147,6 +149,15 @@ int ovh_prefetch(ovh_ctx* ctx, size_t n, const uint8_t* sigs, const uint8_t* has
 int ovh_cache_config(ovh_ctx* ctx, size_t capacity);
 /* stats[0] = hits, stats[1] = misses (fixed-size triples not in the cache), stats[2] = entries. */
 int ovh_cache_stats(ovh_ctx* ctx, uint64_t stats[3]);
+/* Same-message batches (ovh_verify_batch / ovh_prefetch on one device): when the n votes of a
+ * call sign at most n / 2 distinct hashes (a round's votes all sign hash(rlp(Vote)), which has no
+ * voter field: consensus.rs:169-175), the batch is checked as prod_g e(sum_{i in g} r_i pk_i, H_g)
+ * e(-G1, sum_i r_i sigma_i) == 1 with one hash_to_G2 and one Miller loop per distinct hash
+ * (per vote only the key and signature checks and r_i pk_i), then bisected per vote on failure;
+ * the codes are the per-call codes as for any batch. Counters since ovh_create: stats[0] such
+ * batches, stats[1] their votes, stats[2] their distinct hashes. The environment variable
+ * OVH_SAMEMSG=0 (read at ovh_create) turns the path off. */
+int ovh_samemsg_stats(ovh_ctx* ctx, uint64_t stats[3]);
 /* Message cache of the per-call verify (ovh_verify, ovh_verify_batch with n = 1): H =
  * hash_to_G2(hash) of the last 256 hashes verified per call, so every later vote on a hash (all
  * votes of a round sign the same hash, consensus.rs:397-416) skips hash_to_G2. stats[0] = hits,
@@ -234,6 +245,13 @@ const char* ovh_stage_name(int stage);
  * read after each phase barrier: copies min(max, nphases + 1) stamps, returns nphases + 1
  * (0 without the flag, <0 on error). */
 int ovh_vm_trace(ovh_ctx* ctx, int prog, uint64_t* stamps, size_t max);
+/* Diagnostics (context created with OVH_FLAG_VM_CLOCK): per workgroup of the last vote / vote_t
+ * launch, (delta s_memtime, delta s_memrealtime) around its VM program -- shader cycles and
+ * 100 MHz ticks, so the clock the kernel held is delta_memtime / delta_realtime x 100 MHz
+ * (MI355X_MICROARCH.md, DVFS give-back). Copies min(max, 2 x workgroups) values, returns
+ * 2 x workgroups (0 without the flag, <0 on error). The stamps go to a buffer nothing else
+ * reads; without the flag no stamp executes. */
+int ovh_vm_clock(ovh_ctx* ctx, uint64_t* stamps, size_t max);
 
 /* Batched helpers used to synthesise workloads on the device; d_sks are 32-byte big-endian
  * scalars (not key files). */

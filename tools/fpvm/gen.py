@@ -33,17 +33,20 @@ WIDTH.update({"votew": 64, "votew_t": 64, "qcpre": 64, "qcmil": 64, "vote1h": 64
               "signg0": 32, "signg1": 32})   # sign: per call a 32-lane slice (r03y: 2,280 -> 2,123 phases, -14% est.)
 WIDTH.update({"sigchk": 16, "pkchk": 16, "g1padd": 8, "vote1": 64, "vote_t1": 64,
               "final1": 64})
-MAX_SLOTS = {"vote": 200, "vote_t": 200, "fold": 256, "final": 2048, "final1": 2048, "vote1": 1200, "vote_t1": 1200,
+# same-message batches (r04): per vote a 16-lane slice, per distinct hash one 16-lane slice for
+# hash_to_G2 and one wave for its Miller loop (the latency of a round's group)
+WIDTH.update({"vsame": 16, "vsame_t": 16, "h2g": 16, "gmil": 64})
+MAX_SLOTS = {"vsame": 400, "vsame_t": 400, "h2g": 400, "gmil": 1200, "vote": 200, "vote_t": 200, "fold": 256, "final": 2048, "final1": 2048, "vote1": 1200, "vote_t1": 1200,
              "votew": 1200, "votew_t": 1200, "qcpre": 1200, "qcmil": 1200, "vote1h": 1200, "vote_t1h": 1200}
 # phases an op may run ahead of its first consumer's earliest start (sched.schedule `hoist`)
-HOIST = {"vote": 250, "vote_t": 250, "final": 50, "vote1": 250, "vote_t1": 250, "final1": 50, "votew": 250,
+HOIST = {"vsame": 250, "vsame_t": 250, "h2g": 250, "gmil": 250, "vote": 250, "vote_t": 250, "final": 50, "vote1": 250, "vote_t1": 250, "final1": 50, "votew": 250,
          "votew_t": 250, "qcpre": 250, "qcmil": 250, "vote1h": 250, "vote_t1h": 250}
-STRETCH = {"final": 1.0, "vote": 1.0, "vote_t": 1.0, "vote1": 1.0, "vote_t1": 1.0, "final1": 1.0, "votew": 1.0,
+STRETCH = {"vsame": 1.0, "vsame_t": 1.0, "h2g": 1.0, "gmil": 1.0, "final": 1.0, "vote": 1.0, "vote_t": 1.0, "vote1": 1.0, "vote_t1": 1.0, "final1": 1.0, "votew": 1.0,
            "votew_t": 1.0, "qcpre": 1.0, "qcmil": 1.0, "vote1h": 1.0, "vote_t1h": 1.0}
 # priority weight of a heavy op against a light one (path length in weighted ops). r03 scan on
 # the cost model (product phase 1.60 us, linear 0.69 us): vote 4 -> 64 estimates 3.29 -> 3.10 ms
 # (a product on the path outweighs any run of light ops); vote_t keeps 2
-HEAVY_W = {"vote": 64}
+HEAVY_W = {"vote": 64, "vsame": 64, "vsame_t": 64, "h2g": 64}
 # list-scheduling priority offsets per program section (ir.Prog.section): the signature's
 # decompression + subgroup check has no successor, so by path length alone it loses every
 # contended phase to the Miller loop and ends up as a latency-bound tail; the offset runs it in
@@ -60,7 +63,7 @@ SEC_BIAS = {"vote_t": {"sig": 1500}}
 # slots would outgrow the LDS budget).
 NOMIX = set(filter(None, os.environ.get(
     "OVH_GEN_NOMIX", "vote,vote_t,vote1,vote_t1,vote1h,vote_t1h,final1,qcpre,qcmil,votew,votew_t,signg0,signg1,"
-    "sigchk,pkchk,pkgen").split(",")))
+    "sigchk,pkchk,pkgen,vsame,vsame_t,h2g,gmil").split(",")))
 # slots: four vote workgroups (4 x 4 slices) and two finals must share a CU's 160 KiB of LDS
 # (ovhip.hip static_assert); vote 159, final 226 slots with these settings
 
@@ -94,7 +97,7 @@ def emit(consts, built, path):
     lines.append("#define VM_NCONST %d" % len(cw))
     lines.append("#define VM_KZERO %d" % KZERO)
     lines.append("#define VM_KTAB %d" % KTAB)
-    for k in ("S_U", "S_SIG", "S_TAU", "S_F", "S_RS", "S_TOTAL"):
+    for k in ("S_U", "S_SIG", "S_TAU", "S_F", "S_RS", "S_TOTAL", "G_U", "G_H", "G_F", "G_PLANES"):
         lines.append("#define VM_%s %d" % (k, getattr(progs, k)))
     lines.append("static const uint32_t VM_CONST_WORDS[%d] = {" % (12 * len(cw)))
     for e in cw:

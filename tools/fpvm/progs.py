@@ -598,3 +598,86 @@ PROGRAMS["qcmil"] = (build_qcmil, QCMIL_IN, [])
 PROGRAMS["votew"] = (build_votew(False), VOTE_IN, VOTE_OUT)
 PROGRAMS["votew_t"] = (build_votew(True), VOTE_T_IN, VOTE_T_OUT)
 PROGRAMS["g1padd"] = (build_g1padd, G1A_IN + G1B_IN, G1_OUT)
+
+# ---------------------------------------------------------------- same-message batches (r04)
+# Every vote of a round signs the same hash (consensus.rs:169-175: Vote has no voter field), so
+# a batch of n votes over G distinct hashes checks
+#   prod_g e(sum_{i in g} r_i pk_i, H_g) * e(-G1, sum_i r_i sigma_i) == 1
+# with one hash_to_G2 and one Miller loop per hash: per vote only the key / signature checks and
+# r_i pk_i (ovhip.hip verify_samemsg_locked).
+VSAME_IN = ["pk_x", "pk_sort", "sig_x0", "sig_x1", "sig_sort"]
+VSAME_OUT = ["pk_ok", "pk_grp", "sig_ok", "sig_grp"]
+VSAME_T_IN = ["pk_X", "pk_Y", "pk_Z", "sig_x0", "sig_x1", "sig_sort"]
+VSAME_T_OUT = ["sig_ok", "sig_grp"]
+# sigma / tau for the MSM (as the vote program), r pk (homogeneous projective) in the first three
+# f planes (the batch's f planes are free on this path until the bisection)
+VSAME_ST = [("q%d" % k, S_SIG + k) for k in range(4)] + [("t%d" % k, S_TAU + k) for k in range(4)] + \
+    [("r%d" % k, S_F + k) for k in range(3)]
+# group slab planes (per distinct hash): u0, u1 | H projective | f = Miller(apk, H)
+G_U, G_H, G_F, G_PLANES = 0, 4, 10, 22
+H2G_IN = ["u00", "u01", "u10", "u11"]
+H2G_OUT = ["h_inf"]
+GMIL_IN = ["pk_X", "pk_Y", "pk_Z"] + g2p_names("h")
+
+
+def build_vsame(table: bool):
+    def build():
+        """vsame / vsame_t: one vote of a same-message batch -- the key's decompression + G1
+        subgroup check (vsame; vsame_t takes a validator-table point), the signature's
+        decompression + G2 subgroup check, r pk = [a] pk + [b] phi(pk) with the vote's RLC value;
+        stores sigma, tau (the MSM's terms) and r pk."""
+        p = Prog("vsame_t" if table else "vsame")
+        a = Alg(p, use_sop=USE_SOP, fast_sqrt=FAST_SQRT_BATCH)
+        R = p.const(R_MONT)
+        outs = []
+        if table:
+            Pp = (p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z"))
+        else:
+            pk_ok, (px, py) = a.g1_decompress(p.input("pk_x") * R, p.input("pk_sort"))
+            Pp = (px, py, p.one)
+            pk_grp, _ = a.g1_in_group(Pp)
+            outs = [pk_ok, pk_grp]
+        p.section = "sig"
+        sx = (p.input("sig_x0") * R, p.input("sig_x1") * R)
+        sig_ok, (qx, qy) = a.g2_decompress(sx, p.input("sig_sort"))
+        Qs = (qx, qy, (p.one, p.zero))
+        sig_grp = a.g2_in_group(Qs)
+        p.section = None
+        rP = a.pt_mul_glv("fp", Pp, a.g1_phi(Pp))
+        for name, v in zip(VSAME_T_OUT if table else VSAME_OUT, outs + [sig_ok, sig_grp]):
+            p.output(name, v)
+        for (name, plane), v in zip(VSAME_ST, affine_pair(a, Qs) + list(rP)):
+            p.store(name, v, plane)
+        return p
+    return build
+
+
+def build_h2g():
+    """H = hash_to_G2(u0, u1) of one distinct hash of a same-message batch -> the group slab's H
+    planes, and the H-is-infinity flag."""
+    p = Prog("h2g")
+    a = Alg(p, use_sop=USE_SOP, fast_sqrt=True)
+    H = a.hash_to_g2((p.input("u00"), p.input("u01")), (p.input("u10"), p.input("u11")))
+    p.output("h_inf", a.f2_is_zero(H[2]))
+    for k, v in enumerate(flat_g2p(H)):
+        p.store("h%d" % k, v, G_H + k)
+    return p
+
+
+def build_gmil():
+    """f_g = Miller(apk_g, H_g) of one distinct hash (apk_g = sum of its votes' r pk, projective)
+    -> the group slab's f planes."""
+    p = Prog("gmil")
+    a = Alg(p, use_sop=USE_SOP)
+    P = (p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z"))
+    H = unflat_g2p([p.input(n) for n in g2p_names("h")])
+    f = a.miller_loop_multi([(P, H)])
+    for k, v in enumerate(flat12(f)):
+        p.store("f%d" % k, v, G_F + k)
+    return p
+
+
+PROGRAMS["vsame"] = (build_vsame(False), VSAME_IN, VSAME_OUT)
+PROGRAMS["vsame_t"] = (build_vsame(True), VSAME_T_IN, VSAME_T_OUT)
+PROGRAMS["h2g"] = (build_h2g, H2G_IN, H2G_OUT)
+PROGRAMS["gmil"] = (build_gmil, GMIL_IN, [])
