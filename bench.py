@@ -298,14 +298,38 @@ def samemsg_probes(ctx, pks) -> dict:
         ts.append(time.perf_counter() - t)
     out["samemsg4096_ms"] = round(float(np.median(ts)) * 1e3, 3)
     out["samemsg4096_verifs_per_s"] = round(n / float(np.median(ts)), 1)
+    # the same call with the same-message path off (OVH_SAMEMSG=0 at context creation): the
+    # distinct-message batch path on the same votes
+    os.environ["OVH_SAMEMSG"] = "0"
+    try:
+        off = Context(torch.cuda.current_device())
+    finally:
+        del os.environ["OVH_SAMEMSG"]
+    assert lib.ovh_verify_batch(off.ptr, n, sg.tobytes(), digest * n, pk.tobytes(),
+                                codes.ctypes.data_as(ctypes.c_void_p)) == 0 and not (codes != 0).any()
+    ts = []
+    for _ in range(3):
+        t = time.perf_counter()
+        assert lib.ovh_verify_batch(off.ptr, n, sg.tobytes(), digest * n, pk.tobytes(),
+                                    codes.ctypes.data_as(ctypes.c_void_p)) == 0
+        ts.append(time.perf_counter() - t)
+    out["samemsg4096_off_ms"] = round(float(np.median(ts)) * 1e3, 3)
+    off.close()
     # ingress: validator 0 is this node; validators 1..99 send their precommits
     nv = 100
     vs = torch.from_numpy(sks_h[:nv].copy()).cuda()
     vpk = dev.sk_to_pk_batch(ctx, vs).cpu().numpy()
-    node = ConsensusCrypto(bytes(sks_h[0]), ctx=Context(torch.cuda.current_device(), flags=FLAG_SK_RAW))
-    node.update_pubkeys([bytes(x) for x in vpk])
-    rts = []
-    for rnd in range(4):
+    rts, rts_off = [], []
+    for rnd in range(8):
+        if rnd in (0, 4):   # rounds 0-3: the same-message path; 4-7: OVH_SAMEMSG=0 (the small-batch path)
+            if rnd:
+                node.ctx.close()
+                os.environ["OVH_SAMEMSG"] = "0"
+            try:
+                node = ConsensusCrypto(bytes(sks_h[0]), ctx=Context(torch.cuda.current_device(), flags=FLAG_SK_RAW))
+            finally:
+                os.environ.pop("OVH_SAMEMSG", None)
+            node.update_pubkeys([bytes(x) for x in vpk])
         msg = rlp_vote(8, rnd, PRECOMMIT, hashlib.sha256(b"round block").digest())
         assert lib.ovh_sm3(msg, len(msg), buf) == 0
         d = buf.raw
@@ -324,9 +348,10 @@ def samemsg_probes(ctx, pks) -> dict:
             raise RuntimeError("ingress round: %d forwarded, %d batches" % (len(fwd), sh.stats["batches"]))
         for m in fwd[:3]:
             ig.overlord_verify(node, ig.SIGNED_VOTE, m)
-        if rnd:
-            rts.append(dt)
+        if rnd % 4:
+            (rts if rnd < 4 else rts_off).append(dt)
     out["round99_ms"] = round(float(np.median(rts)) * 1e3, 3)
+    out["round99_off_ms"] = round(float(np.median(rts_off)) * 1e3, 3)
     node.ctx.close()
     return out
 

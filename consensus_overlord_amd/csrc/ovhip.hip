@@ -1754,6 +1754,43 @@ __global__ __launch_bounds__(WG) void k_parse_pk_list(uint32_t n, const uint8_t*
   codes[i] = e;
 }
 
+// aggregate_signatures' key validation on the VM (program pkdec: the decompression alone, no
+// subgroup check -- the keys are only parsed, consensus.rs:435-436), one 48-byte key per 4-lane
+// slice: codes[i] = BLST_SUCCESS or the parse failure as k_parse_pk_list reports it (bad
+// encoding, off the curve, x = 0; infinity parses).
+constexpr uint32_t PKDEC_STRIDE_W = align128w(VM_PKDEC_NSLOTS * 12 + 4);
+__global__ __launch_bounds__(64) void k_vm_pkdec(uint32_t n, VmDev prog, const uint32_t* __restrict__ cst_g,
+                                                 const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+                                                 int32_t* __restrict__ codes) {
+  constexpr uint32_t W = VM_PKDEC_W, SL = 64 / W;
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / W, lane = threadIdx.x % W;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * PKDEC_STRIDE_W;
+  uint32_t* hdr = slots + VM_PKDEC_NSLOTS * 12;
+  const uint32_t i = blockIdx.x * SL + slice;
+  const bool active = i < n;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active && lane == 0) {
+    uint32_t x[12], bad, inf, sort, xz;
+    parse_hdr(data + off[i], 48, x, x, bad, inf, sort, xz);
+    slot_put(slots, VM_PKDEC_IN[VM_PKCHK_IN_PK_X], x);
+    slot_flag(slots, VM_PKDEC_IN[VM_PKCHK_IN_PK_SORT], sort);
+    hdr[0] = bad | inf << 1 | xz << 2;
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_PKDEC_NPHASES, W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  if (active && lane == 0) {
+    const uint32_t pf = hdr[0];
+    int32_t c = BLST_SUCCESS;
+    if (pf & 1) c = BLST_BAD_ENCODING;
+    else if (!(pf & 2) && !slot_flag_get(slots, VM_PKDEC_OUT[VM_PKDEC_OUT_PK_OK])) c = BLST_POINT_NOT_ON_CURVE;
+    else if (!(pf & 2) && (pf & 4)) c = BLST_POINT_NOT_IN_GROUP;  // x = 0: (0, +-2) has order 3
+    codes[i] = c;
+  }
+}
+
 __global__ __launch_bounds__(WG) void k_sum_g1(uint32_t n, Slab pts, uint32_t* out_jac /*36 words*/, uint8_t* out48) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   G1J acc, x;
@@ -1918,7 +1955,7 @@ struct ovh_ctx {
   // Fp-VM programs + constant table in device memory
   // same-message batches (verify_samemsg_locked): programs, per slot the group slab (G_PLANES
   // planes + the H-is-infinity words, gcap entries); OVH_SAMEMSG=0 turns the path off
-  VmDev vm_vsame{}, vm_vsame_t{}, vm_h2g{}, vm_gmil{};
+  VmDev vm_vsame{}, vm_vsame_t{}, vm_h2g{}, vm_gmil{}, vm_pkdec{};
   uint32_t* gslab[OVH_BATCH_SLOTS] = {};
   uint32_t gcap[OVH_BATCH_SLOTS] = {};
   bool samemsg = true;
@@ -2001,6 +2038,8 @@ static constexpr size_t LDS_VSAME = ((size_t)SLOT_BASE_W + VM_SLICES * (size_t)V
 static constexpr size_t LDS_H2G = ((size_t)SLOT_BASE_W + VM_SLICES * (size_t)H2G_STRIDE_W) * 4;
 static constexpr size_t LDS_GMIL = ((size_t)SLOT_BASE_W + (size_t)VM_GMIL_NSLOTS * 12) * 4;
 static_assert(LDS_VSAME <= 64 * 1024 && LDS_H2G <= 64 * 1024 && LDS_GMIL + 16 <= 64 * 1024, "same-message LDS");
+static constexpr size_t LDS_PKDEC = ((size_t)SLOT_BASE_W + (64 / VM_PKDEC_W) * (size_t)PKDEC_STRIDE_W) * 4;
+static_assert(LDS_PKDEC <= 64 * 1024 && VM_PKDEC_NIN == 2, "pkdec LDS / shape");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
 // allocation granules assumed)
 constexpr size_t lds_granule(size_t b) { return (b + 1023) / 1024 * 1024; }
@@ -2093,6 +2132,8 @@ static int vm_init(ovh_ctx* c) {
                 VM_VSAME_T_NIN, VM_VSAME_T_OUT, VM_VSAME_T_NOUT));
   CHK(vm_upload(c, c->vm_h2g, VM_H2G_CODE, VM_H2G_NPHASES, VM_H2G_W, VM_H2G_NW, VM_H2G_IN, VM_H2G_NIN, VM_H2G_OUT,
                 VM_H2G_NOUT));
+  CHK(vm_upload(c, c->vm_pkdec, VM_PKDEC_CODE, VM_PKDEC_NPHASES, VM_PKDEC_W, VM_PKDEC_NW, VM_PKDEC_IN, VM_PKDEC_NIN,
+                VM_PKDEC_OUT, VM_PKDEC_NOUT));
   CHK(vm_upload(c, c->vm_gmil, VM_GMIL_CODE, VM_GMIL_NPHASES, VM_GMIL_W, VM_GMIL_NW, VM_GMIL_IN, VM_GMIL_NIN, nullptr, 0));
   CHK(vm_upload(c, c->vm_g1padd, VM_G1PADD_CODE, VM_G1PADD_NPHASES, VM_G1PADD_W, VM_G1PADD_NW, VM_G1PADD_IN,
                 VM_G1PADD_NIN, VM_G1PADD_OUT, VM_G1PADD_NOUT));
@@ -2812,21 +2853,28 @@ static int verify_samemsg_locked(ovh_ctx* c, size_t n, uint8_t* d, size_t t, con
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
   int reg = 0;
   uint32_t m = (G + 3) / 4;
+  k_samemsg_fix<<<nblk(n), WG, 0, fst>>>(N, gid, ghinf, dc, P);
+  // the per-hash key sums, Miller loops and their fold on the side stream, beside the MSM
+  if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+  const hipStream_t xs = c->xstream;
+  HIPCHK(hipEventRecord(c->ev_x[2], fst));
+  HIPCHK(hipStreamWaitEvent(xs, c->ev_x[2], 0));
   {
-    StageScope p(c, ST_FOLD, fst);
-    k_samemsg_fix<<<nblk(n), WG, 0, fst>>>(N, gid, ghinf, dc, P);
+    StageScope p(c, ST_FOLD, xs);
     for (size_t l = 0; l + 1 < pl.level_off.size(); ++l) {
       const uint32_t a = pl.level_off[l], np = pl.level_off[l + 1] - a;
-      k_vm_g1pairs<<<(np + 64 / VM_G1PADD_W - 1) / (64 / VM_G1PADD_W), 64, LDS_G1PADD, fst>>>(
+      k_vm_g1pairs<<<(np + 64 / VM_G1PADD_W - 1) / (64 / VM_G1PADD_W), 64, LDS_G1PADD, xs>>>(
           np, c->vm_g1padd, G1PADD_STRIDE_W, c->vm_consts, pairs + 2 * (size_t)a, P);
     }
-    k_vm_gmil<<<G, 64, LDS_GMIL, fst>>>(G, c->vm_gmil, c->vm_consts, head, P, g);
-    k_vm_fold<VM_FOLD_UNITS><<<(m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, fst>>>(
+    k_vm_gmil<<<G, 64, LDS_GMIL, xs>>>(G, c->vm_gmil, c->vm_consts, head, P, g);
+    k_vm_fold<VM_FOLD_UNITS><<<(m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, xs>>>(
         G, c->vm_fold, c->vm_consts, Slab{g.p + (size_t)VM_G_F * 12 * g.cap, g.cap}, Slab{nullptr, 0},
         region_F(c, slot, 0), nullptr);
   }
-  CHK(fold_down(c, slot, fst, 1, &reg, &m, 4));
+  CHK(fold_down(c, slot, xs, 1, &reg, &m, 4));
   CHK(enqueue_msm(c, fst, slot, N, dc));
+  HIPCHK(hipEventRecord(c->ev_x[3], xs));
+  HIPCHK(hipStreamWaitEvent(fst, c->ev_x[3], 0));
   int32_t* verdict = c->result + RES_BATCH + slot;
   enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict, msm_S(c, slot));
   {
@@ -3776,7 +3824,15 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
     // map onto distinct hardware queues at HIP's default of four (GPU_MAX_HW_QUEUES)
     if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
     HIPCHK(hipStreamWaitEvent(c->xstream, c->ev_x[2], 0));
-    k_parse_pk_list<<<nblk(n), WG, 0, c->xstream>>>((uint32_t)n, dp, po, pl, c->scr_pk, ppts);
+    bool keys48 = true;
+    for (size_t i = 0; i < n; ++i) keys48 = keys48 && pk_lens[i] == 48;
+    if (keys48) {  // compressed keys: the decompression on the VM (r04; was one lane per key)
+      constexpr uint32_t KSL = 64 / VM_PKDEC_W;
+      k_vm_pkdec<<<(uint32_t)((n + KSL - 1) / KSL), 64, LDS_PKDEC, c->xstream>>>((uint32_t)n, c->vm_pkdec,
+                                                                                c->vm_consts, dp, po, c->scr_pk);
+    } else {  // other encodings (uncompressed keys: an on-curve check, no square root)
+      k_parse_pk_list<<<nblk(n), WG, 0, c->xstream>>>((uint32_t)n, dp, po, pl, c->scr_pk, ppts);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev_x[3], c->xstream));
     const int gc = (c->flags & OVH_FLAG_AGG_NO_GROUPCHECK) ? 0 : 1;

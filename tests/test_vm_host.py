@@ -251,3 +251,35 @@ def test_percall_programs_on_interpreter(hx, built, golden_votes, any_all):  # n
     run("pkgen", {"c0": 0, "c1": 1, "c2": 0}, 0xFEDCBA9876543210)
     o = run("qcmil", mi)
     assert run("final1", {"f%d" % j: o["st:f%d" % j] for j in range(12)}) == {"ok": 1}
+
+
+@pytest.mark.parametrize("any_all", [0, 1])
+def test_samemsg_programs_on_interpreter(hx, built, golden_votes, any_all):  # noqa: F811
+    """The same-message programs through the interpreter == simulator,
+    and the simulator == the oracle (gen.check_samemsg: sigma, tau, r pk, hash_to_G2, the Miller
+    loop of the key sum, pkdec's key validation)."""
+    consts, progs_ = built
+    bls = gen._oracle()
+    with open(os.path.join(ROOT, "tests", "golden", "golden_v1.json")) as fh:
+        g = json.load(fh)
+    if any_all == 0:
+        gen.check_samemsg(progs_, bls, g)
+    r = 0xC2B2AE3D27D4EB4F
+
+    def run(name, inp, scalar=0):
+        _, sc, words, _, _ = progs_[name]
+        sim = sched.simulate(sc, words, inp, scalar)
+        assert_same(run_vm(hx, consts, sc, words, inp, scalar, any_all), sim, name)
+        return sim
+    for inp in golden_votes:
+        o = run("vsame", {n: inp[n] for n in progs.VSAME_IN}, r)
+        run("pkdec", {n: inp[n] for n in progs.PKCHK_IN})
+    pk = bls.g1_from_bytes(bytes.fromhex(g["keys"][0]["pk"]))
+    inp = golden_votes[0]
+    tin = {n: inp[n] for n in ("sig_x0", "sig_x1", "sig_sort")}
+    tin.update(pk_X=pk[0] * 5 % P, pk_Y=pk[1] * 5 % P, pk_Z=5)
+    run("vsame_t", tin, r)
+    h = run("h2g", {n: inp[n] for n in progs.H2G_IN})
+    o = run("vsame", {n: inp[n] for n in progs.VSAME_IN}, r)
+    mi = dict(zip(progs.GMIL_IN, [o["st:r%d" % j] for j in range(3)] + [h["st:h%d" % j] for j in range(6)]))
+    run("gmil", mi)

@@ -35,7 +35,7 @@ WIDTH.update({"sigchk": 16, "pkchk": 16, "g1padd": 8, "vote1": 64, "vote_t1": 64
               "final1": 64})
 # same-message batches (r04): per vote a 16-lane slice, per distinct hash one 16-lane slice for
 # hash_to_G2 and one wave for its Miller loop (the latency of a round's group)
-WIDTH.update({"vsame": 16, "vsame_t": 16, "h2g": 16, "gmil": 64})
+WIDTH.update({"vsame": 16, "vsame_t": 16, "h2g": 16, "gmil": 64, "pkdec": 4})
 MAX_SLOTS = {"vsame": 400, "vsame_t": 400, "h2g": 400, "gmil": 1200, "vote": 200, "vote_t": 200, "fold": 256, "final": 2048, "final1": 2048, "vote1": 1200, "vote_t1": 1200,
              "votew": 1200, "votew_t": 1200, "qcpre": 1200, "qcmil": 1200, "vote1h": 1200, "vote_t1h": 1200}
 # phases an op may run ahead of its first consumer's earliest start (sched.schedule `hoist`)
@@ -63,7 +63,7 @@ SEC_BIAS = {"vote_t": {"sig": 1500}}
 # slots would outgrow the LDS budget).
 NOMIX = set(filter(None, os.environ.get(
     "OVH_GEN_NOMIX", "vote,vote_t,vote1,vote_t1,vote1h,vote_t1h,final1,qcpre,qcmil,votew,votew_t,signg0,signg1,"
-    "sigchk,pkchk,pkgen,vsame,vsame_t,h2g,gmil").split(",")))
+    "sigchk,pkchk,pkgen,vsame,vsame_t,h2g,gmil,pkdec").split(",")))
 # slots: four vote workgroups (4 x 4 slices) and two finals must share a CU's 160 KiB of LDS
 # (ovhip.hip static_assert); vote 159, final 226 slots with these settings
 
@@ -260,7 +260,63 @@ def check(built):
     check_vote1h(built, bls, g)
     check_pkgen(built, bls, g)
     check_signg(built, bls, g)
+    check_samemsg(built, bls, g)
     print("fpvm check: vote/vote_t/rs/fold/final/MSM/sigchk/pkchk/g1padd programs match the oracle and their DAGs")
+
+
+def check_samemsg(built, bls, g):
+    """Same-message programs (ovhip.hip verify_samemsg_locked): vsame / vsame_t store the golden
+    sigma, tau = -psi^2(sigma) and r pk (projective), h2g stores hash_to_G2(hash) (projective),
+    gmil(r pk, H) has the final exponentiation of Miller(r pk, H) (the vote program's f); pkdec
+    accepts golden keys and rejects the off-curve one."""
+    r = 0xC2B2AE3D27D4EB4F
+    for v, k in list(zip(g["votes"], g["keys"]))[:2]:
+        pkb, sigb, h = bytes.fromhex(k["pk"]), bytes.fromhex(v["sig"]), bytes.fromhex(v["digest"])
+        inp = vote_inputs(bls, pkb, sigb, h)
+        prog, sc, words, ins, outs = built["vsame"]
+        vin = {n: inp[n] for n in ins}
+        vals = prog.evaluate(vin, r)
+        got = {n: vals[i] for n, i in prog.outputs.items()}
+        assert sched.simulate(sc, words, vin, r) == got, "vsame: simulated"
+        assert [got[n] for n in outs] == [1, 1, 1, 1], "vsame: flags"
+        sig = bls.g2_from_bytes(sigb)
+        pk = bls.g1_from_bytes(pkb)
+        assert (got["st:q0"], got["st:q1"], got["st:q2"], got["st:q3"]) == (sig[0][0], sig[0][1], sig[1][0], sig[1][1])
+        tau = bls.pt_neg(bls.Fp2Ops, bls.g2_psi(bls.g2_psi(sig)))
+        assert (got["st:t0"], got["st:t1"], got["st:t2"], got["st:t3"]) == (tau[0][0], tau[0][1], tau[1][0], tau[1][1])
+        X, Y, Z = (got["st:r%d" % j] for j in range(3))
+        zi = pow(Z, -1, P)
+        rP = bls.pt_mul(bls.FpOps, pk, alg.rlc_scalar(r))
+        assert (X * zi % P, Y * zi % P) == rP, "vsame: r pk"
+        tprog, tsc, twords, tins, touts = built["vsame_t"]
+        tin = {n: inp[n] for n in ("sig_x0", "sig_x1", "sig_sort")}
+        tin.update(pk_X=pk[0] * 3 % P, pk_Y=pk[1] * 3 % P, pk_Z=3)
+        tv = tprog.evaluate(tin, r)
+        tgot = {n: tv[i] for n, i in tprog.outputs.items()}
+        assert sched.simulate(tsc, twords, tin, r) == tgot, "vsame_t: simulated"
+        Xt, Yt, Zt = (tgot["st:r%d" % j] for j in range(3))
+        assert (Xt * pow(Zt, -1, P) % P, Yt * pow(Zt, -1, P) % P) == rP, "vsame_t: r pk"
+        hprog, hsc, hwords, hins, _ = built["h2g"]
+        hin = {n: inp[n] for n in hins}
+        hv = hprog.evaluate(hin)
+        hgot = {n: hv[i] for n, i in hprog.outputs.items()}
+        assert sched.simulate(hsc, hwords, hin) == hgot, "h2g: simulated"
+        Hp = [hgot["st:h%d" % j] for j in range(6)]
+        assert _to_aff(bls, Hp) == bls.hash_to_g2(h) and hgot["h_inf"] == 0, "h2g: H"
+        mprog, msc, mwords, mins, _ = built["gmil"]
+        minp = dict(zip(mins, [X, Y, Z] + Hp))
+        mv = mprog.evaluate(minp)
+        mgot = {n: mv[i] for n, i in mprog.outputs.items()}
+        assert sched.simulate(msc, mwords, minp) == mgot, "gmil: simulated"
+        f = progs.unflat12([mgot["st:f%d" % j] for j in range(12)])
+        assert bls.f12_eq(bls.final_exponentiation_x_chain(f),
+                          bls.final_exponentiation_x_chain(bls.miller_loop(rP, bls.hash_to_g2(h)))), "gmil: f"
+    dprog, dsc, dwords, dins, _ = built["pkdec"]
+    named = {c["name"]: bytes.fromhex(c["pk"]) for c in g["verify"]}
+    for pkb, ok in [(bytes.fromhex(k["pk"]), 1) for k in g["keys"][:2]] + [(named["pk_not_on_curve"], 0)]:
+        din = {"pk_x": int.from_bytes(bytes([pkb[0] & 0x1F]) + pkb[1:48], "big") * RINV, "pk_sort": (pkb[0] >> 5) & 1}
+        dv = dprog.evaluate(din)
+        assert dv[dprog.outputs["pk_ok"]] == ok and sched.simulate(dsc, dwords, din) == {"pk_ok": ok}, "pkdec"
 
 
 def check_sigchk(built, bls, g):

@@ -415,6 +415,20 @@ def build_pkchk():
     return p
 
 
+PKDEC_OUT = ["pk_ok"]
+
+
+def build_pkdec():
+    """aggregate_signatures' key validation (consensus.rs:435-436: the keys are only parsed):
+    the 48-byte key's decompression alone -- x^3 + 4 a square -- with no subgroup check."""
+    p = Prog("pkdec")
+    a = Alg(p, use_sop=USE_SOP, fast_sqrt=True)
+    R = p.const(R_MONT)
+    pk_ok, _ = a.g1_decompress(p.input("pk_x") * R, p.input("pk_sort"))
+    p.output("pk_ok", pk_ok)
+    return p
+
+
 G1A_IN = ["a%d" % k for k in range(3)]
 G1B_IN = ["b%d" % k for k in range(3)]
 G1_OUT = ["s%d" % k for k in range(3)]
@@ -677,6 +691,7 @@ def build_gmil():
     return p
 
 
+PROGRAMS["pkdec"] = (build_pkdec, PKCHK_IN, PKDEC_OUT)
 PROGRAMS["vsame"] = (build_vsame(False), VSAME_IN, VSAME_OUT)
 PROGRAMS["vsame_t"] = (build_vsame(True), VSAME_T_IN, VSAME_T_OUT)
 PROGRAMS["h2g"] = (build_h2g, H2G_IN, H2G_OUT)
