@@ -1570,6 +1570,31 @@ __global__ __launch_bounds__(64) void k_apk_finish(Slab in, Slab out, uint32_t* 
   }
 }
 
+// verify_aggregated_signature when some key is outside G1 (BlsPublicKey::aggregate does not
+// group-check; blst's verify checks the aggregated key, consensus.rs:371,378-380): program g1grp
+// on element 0 of `apk` (one 16-lane slice) -> PKF_GRP in flags[0] when the sum is not in G1
+// (an infinite sum keeps PKF_INF, which takes precedence in k_vm_qcmil).
+constexpr uint32_t G1GRP_STRIDE_W = align256w(VM_G1GRP_NSLOTS * 12);
+__global__ __launch_bounds__(64) void k_vm_g1grp(VmDev prog, const uint32_t* __restrict__ cst_g, Slab apk,
+                                                 uint32_t* __restrict__ flags) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  const uint32_t slice = threadIdx.x / VM_G1GRP_W, lane = threadIdx.x % VM_G1GRP_W;
+  uint32_t* slots = lds + SLOT_BASE_W;
+  const bool active = slice == 0;
+  load_consts(cst, cst_g, VM_NCONST);
+  if (active && lane < 3) {
+    Fp v;
+    apk.ld(v, lane, 0);
+    slot_put(slots, VM_G1GRP_IN[lane], v.v);
+  }
+  __syncthreads();
+  vm::run(prog.code, VM_G1GRP_NPHASES, VM_G1GRP_W, lane, active, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  if (active && lane == 0 && !(flags[0] & PKF_INF) && !slot_flag_get(slots, VM_G1GRP_OUT[VM_G1GRP_OUT_PK_GRP]))
+    flags[0] |= PKF_GRP;
+}
+
 // QC batch: one workgroup per QC, apk = sum of the table keys selected by the QC's voter list
 // (sorted-order indices, CSR): each lane sums a strided share (Jacobian), then a 6-level LDS tree;
 // out = homogeneous projective (X Z : Y : Z^3); flags: PKF_INF when the sum is O.
@@ -1955,7 +1980,7 @@ struct ovh_ctx {
   // Fp-VM programs + constant table in device memory
   // same-message batches (verify_samemsg_locked): programs, per slot the group slab (G_PLANES
   // planes + the H-is-infinity words, gcap entries); OVH_SAMEMSG=0 turns the path off
-  VmDev vm_vsame{}, vm_vsame_t{}, vm_h2g{}, vm_gmil{}, vm_pkdec{};
+  VmDev vm_vsame{}, vm_vsame_t{}, vm_h2g{}, vm_gmil{}, vm_pkdec{}, vm_g1grp{};
   uint32_t* gslab[OVH_BATCH_SLOTS] = {};
   uint32_t gcap[OVH_BATCH_SLOTS] = {};
   bool samemsg = true;
@@ -2040,6 +2065,8 @@ static constexpr size_t LDS_GMIL = ((size_t)SLOT_BASE_W + (size_t)VM_GMIL_NSLOTS
 static_assert(LDS_VSAME <= 64 * 1024 && LDS_H2G <= 64 * 1024 && LDS_GMIL + 16 <= 64 * 1024, "same-message LDS");
 static constexpr size_t LDS_PKDEC = ((size_t)SLOT_BASE_W + (64 / VM_PKDEC_W) * (size_t)PKDEC_STRIDE_W) * 4;
 static_assert(LDS_PKDEC <= 64 * 1024 && VM_PKDEC_NIN == 2, "pkdec LDS / shape");
+static constexpr size_t LDS_G1GRP = ((size_t)SLOT_BASE_W + (size_t)G1GRP_STRIDE_W) * 4;
+static_assert(LDS_G1GRP <= 64 * 1024 && VM_G1GRP_NIN == 3, "g1grp LDS / shape");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
 // allocation granules assumed)
 constexpr size_t lds_granule(size_t b) { return (b + 1023) / 1024 * 1024; }
@@ -2132,6 +2159,8 @@ static int vm_init(ovh_ctx* c) {
                 VM_VSAME_T_NIN, VM_VSAME_T_OUT, VM_VSAME_T_NOUT));
   CHK(vm_upload(c, c->vm_h2g, VM_H2G_CODE, VM_H2G_NPHASES, VM_H2G_W, VM_H2G_NW, VM_H2G_IN, VM_H2G_NIN, VM_H2G_OUT,
                 VM_H2G_NOUT));
+  CHK(vm_upload(c, c->vm_g1grp, VM_G1GRP_CODE, VM_G1GRP_NPHASES, VM_G1GRP_W, VM_G1GRP_NW, VM_G1GRP_IN, VM_G1GRP_NIN,
+                VM_G1GRP_OUT, VM_G1GRP_NOUT));
   CHK(vm_upload(c, c->vm_pkdec, VM_PKDEC_CODE, VM_PKDEC_NPHASES, VM_PKDEC_W, VM_PKDEC_NW, VM_PKDEC_IN, VM_PKDEC_NIN,
                 VM_PKDEC_OUT, VM_PKDEC_NOUT));
   CHK(vm_upload(c, c->vm_gmil, VM_GMIL_CODE, VM_GMIL_NPHASES, VM_GMIL_W, VM_GMIL_NW, VM_GMIL_IN, VM_GMIL_NIN, nullptr, 0));
@@ -4061,7 +4090,8 @@ static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_l
     *code = OVH_ERR_PUBKEY;
     return 0;
   }
-  if (fl & PKF_GRP) return 1;
+  // a key outside G1 (r04: on the VM; was the one-lane k_verify_agg): the sum is group-checked
+  // below (k_vm_g1grp), as blst's verify checks the aggregated key
   uint32_t* qflags = c->qc_buf + (size_t)3 * 12 * c->qc_cap;
   {
     constexpr uint32_t SL = 64 / VM_G1PADD_W;
@@ -4075,6 +4105,8 @@ static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_l
       base = dst;
     }
     k_apk_finish<<<1, 64, 0, c->stream>>>(Slab{c->qt_buf + base, c->qt_cap}, Slab{c->qc_buf, c->qc_cap}, qflags);
+    if (fl & PKF_GRP)
+      k_vm_g1grp<<<1, 64, LDS_G1GRP, c->stream>>>(c->vm_g1grp, c->vm_consts, Slab{c->qc_buf, c->qc_cap}, qflags);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_x[3], 0));
@@ -4276,7 +4308,7 @@ static int qc_batch_locked(ovh_ctx* c, size_t nq, const uint8_t* sigs, const uin
     } else if (!cnt) {
       codes[q] = BLST_AGGR_TYPE_MISMATCH;
     } else if (fl & PKF_GRP) {
-      // a key outside G1: the sum's own group check decides -> the exact single-QC path
+      // a key outside G1: the sum's own group check decides -> the single-QC path (k_vm_g1grp)
       std::vector<uint8_t> cat;
       std::vector<size_t> lens;
       for (size_t k = start; k < ent.size(); ++k) {
@@ -4285,7 +4317,7 @@ static int qc_batch_locked(ovh_ctx* c, size_t nq, const uint8_t* sigs, const uin
       }
       ent.resize(start);
       const int r =
-          verify_aggregated_locked(c, sigs + 96 * q, 96, hashes + 32 * q, 32, cat.data(), lens.data(), cnt, true);
+          verify_aggregated_locked(c, sigs + 96 * q, 96, hashes + 32 * q, 32, cat.data(), lens.data(), cnt);
       if (r >= OVH_ERR_ARG) return r;
       codes[q] = r;
     } else {

@@ -102,3 +102,63 @@ def test_aggregate_pks_vm_matches_oracle(golden):
         assert got == code, (len(voters), got, code)
         if code == 0:
             assert out.raw == want, len(voters)
+
+
+def _order11_point():
+    """A point of order 11 on E(Fp) (11 divides the G1 cofactor (x - 1)^2 / 3): outside G1, and
+    its x is not 0 (the order-3 points (0, +-2) do not parse, DESIGN.md assumption 5)."""
+    import bls12_381 as bls
+    h1 = (bls.X - 1) ** 2 // 3
+    assert h1 % 121 == 0   # the 11-part of E(Fp) has exponent 11: [h1 / 121 r] P has order 1 or 11
+    x = 5
+    while True:
+        y = bls.fp_sqrt((x ** 3 + 4) % bls.P)
+        if y is not None:
+            T = bls.pt_mul(bls.FpOps, (x, y), h1 // 121 * bls.R)
+            if T is not None:
+                assert bls.pt_mul(bls.FpOps, T, 11) is None
+                return T
+        x += 1
+
+
+def test_aggregated_key_outside_g1_checked_on_the_sum():
+    """verify_aggregated_signature checks the SUM of the keys (BlsPublicKey::aggregate does not
+    group-check, blst's verify checks the aggregated key: consensus.rs:371,378-380): keys A + T
+    and B - T (T of order 11, both outside G1) sum into G1 and verify; either alone, or with B,
+    does not (POINT_NOT_IN_GROUP) -- on the VM (k_vm_g1grp), per call and in a QC batch, as the
+    C oracle."""
+    import bls12_381 as bls
+    import orc
+    import consensus_overlord_amd as coa
+    F = bls.FpOps
+    cc = coa.ConsensusCrypto(bytes.fromhex("4d" * 32))
+    h = bytes.fromhex("5e" * 32)
+    sa, sb = 0x1234567 * 0x9E3779B97F4A7C15 % bls.R, 0x7654321 * 0xC2B2AE3D27D4EB4F % bls.R
+    A, B = bls.sk_to_pk(sa), bls.sk_to_pk(sb)
+    T = _order11_point()
+    K1 = bls.g1_compress(bls.pt_add(F, A, T))
+    K2 = bls.g1_compress(bls.pt_add(F, B, bls.pt_neg(F, T)))
+    Bc = bls.g1_compress(B)
+    agg = orc.aggregate_sigs([orc.sign(sa.to_bytes(32, "big"), h)[1], orc.sign(sb.to_bytes(32, "big"), h)[1]],
+                             [bls.g1_compress(A), Bc])[1]
+    cases = [[K1, K2], [K1], [K1, Bc], [K2, K1]]
+    want = [orc.verify_aggregated(agg, h, ks) for ks in cases]
+    assert want == [0, 3, 3, 0]
+
+    def vagg(ks):
+        lens = (ctypes.c_size_t * len(ks))(*[48] * len(ks))
+        return cc.lib.ovh_verify_aggregated(cc.ctx.ptr, agg, 96, h, 32, b"".join(ks), lens, len(ks))
+    assert [vagg(ks) for ks in cases] == want
+    # the same QCs through the validator table (ovh_verify_qc_batch)
+    table = [K1, K2, Bc, bls.g1_compress(A)]
+    cc.update_pubkeys(table)
+    skeys = sorted(table)
+    bms = []
+    for ks in cases:
+        bm = bytearray(1)
+        for k in ks:
+            i = skeys.index(k)
+            bm[0] |= 0x80 >> i
+        bms.append(bytes(bm))
+    got = cc.verify_qc_batch([agg] * len(cases), [h] * len(cases), bms)
+    assert got.tolist() == want

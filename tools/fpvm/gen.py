@@ -35,7 +35,7 @@ WIDTH.update({"sigchk": 16, "pkchk": 16, "g1padd": 8, "vote1": 64, "vote_t1": 64
               "final1": 64})
 # same-message batches (r04): per vote a 16-lane slice, per distinct hash one 16-lane slice for
 # hash_to_G2 and one wave for its Miller loop (the latency of a round's group)
-WIDTH.update({"vsame": 16, "vsame_t": 16, "h2g": 16, "gmil": 64, "pkdec": 4})
+WIDTH.update({"vsame": 16, "vsame_t": 16, "h2g": 16, "gmil": 64, "pkdec": 4, "g1grp": 16})
 MAX_SLOTS = {"vsame": 400, "vsame_t": 400, "h2g": 400, "gmil": 1200, "vote": 200, "vote_t": 200, "fold": 256, "final": 2048, "final1": 2048, "vote1": 1200, "vote_t1": 1200,
              "votew": 1200, "votew_t": 1200, "qcpre": 1200, "qcmil": 1200, "vote1h": 1200, "vote_t1h": 1200}
 # phases an op may run ahead of its first consumer's earliest start (sched.schedule `hoist`)
@@ -63,7 +63,7 @@ SEC_BIAS = {"vote_t": {"sig": 1500}}
 # slots would outgrow the LDS budget).
 NOMIX = set(filter(None, os.environ.get(
     "OVH_GEN_NOMIX", "vote,vote_t,vote1,vote_t1,vote1h,vote_t1h,final1,qcpre,qcmil,votew,votew_t,signg0,signg1,"
-    "sigchk,pkchk,pkgen,vsame,vsame_t,h2g,gmil,pkdec").split(",")))
+    "sigchk,pkchk,pkgen,vsame,vsame_t,h2g,gmil,pkdec,g1grp").split(",")))
 # slots: four vote workgroups (4 x 4 slices) and two finals must share a CU's 160 KiB of LDS
 # (ovhip.hip static_assert); vote 159, final 226 slots with these settings
 

@@ -416,6 +416,20 @@ def build_pkchk():
 
 
 PKDEC_OUT = ["pk_ok"]
+G1GRP_IN = ["pk_X", "pk_Y", "pk_Z"]
+G1GRP_OUT = ["pk_grp"]
+
+
+def build_g1grp():
+    """verify_aggregated_signature with keys outside G1 (BlsPublicKey::aggregate does not
+    group-check, blst's verify checks the SUM, consensus.rs:371,378-380): the G1 subgroup check of
+    the aggregated key (projective)."""
+    p = Prog("g1grp")
+    a = Alg(p, use_sop=USE_SOP)
+    grp, _ = a.g1_in_group((p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z")))
+    p.output("pk_grp", grp)
+    return p
+
 
 
 def build_pkdec():
@@ -692,6 +706,7 @@ def build_gmil():
 
 
 PROGRAMS["pkdec"] = (build_pkdec, PKCHK_IN, PKDEC_OUT)
+PROGRAMS["g1grp"] = (build_g1grp, G1GRP_IN, G1GRP_OUT)
 PROGRAMS["vsame"] = (build_vsame(False), VSAME_IN, VSAME_OUT)
 PROGRAMS["vsame_t"] = (build_vsame(True), VSAME_T_IN, VSAME_T_OUT)
 PROGRAMS["h2g"] = (build_h2g, H2G_IN, H2G_OUT)
