@@ -49,10 +49,15 @@ OVH_FLAG_VM_CLOCK = 0x20
 #  PEAK_FULLRATE  the theoretical full-rate 32-bit VALU lane rate, 256 CU x 64 lanes/clk x
 #                 2.4 GHz = 3.93e13 lane-ops/s (one wave instruction per 4 cycles per SIMD)
 #  PEAK_MAD_U64   the measured v_mad_u64_u32 lane-op rate (tools/ubench/int_rates.hip, best
-#                 occupancy; profiles/r04_int_rates.json), at the clock that run held
+#                 occupancy: 8 waves per SIMD, 4.14 cycles per wave instruction;
+#                 profiles/r04_int_rates.json), at the clock that run held
+#  PEAK_MAD_1WAVE_CHAIN  the same instruction on one dependent chain at one wave per SIMD (the
+#                 product's order at the vote kernel's occupancy: 5.93 cycles)
+# (r01-r03 used 2.9143e13 from a ubench whose loop carried an s_nop between consecutive mads.)
 PEAK_FULLRATE = 256 * 64 * 2.4e9
-PEAK_MAD_U64 = 2.9143e13
-PEAK_MAD_U64_CLOCK_GHZ = None
+PEAK_MAD_U64 = 3.7584e13
+PEAK_MAD_U64_CLOCK_GHZ = 2.371
+PEAK_MAD_1WAVE_CHAIN = 2.6448e13
 W_V_CANON = 18300   # algorithmic Montgomery products per verification
 W_MSM = 350         # the Pippenger share of sum r_i sigma_i (the k_msm_* kernels)
 STAGE_TO_WORK = {"hash_to_field": "hash_to_field", "vote": "vote", "fold": "fold_per_partial",
@@ -298,6 +303,9 @@ def samemsg_probes(ctx, pks) -> dict:
         ts.append(time.perf_counter() - t)
     out["samemsg4096_ms"] = round(float(np.median(ts)) * 1e3, 3)
     out["samemsg4096_verifs_per_s"] = round(n / float(np.median(ts)), 1)
+    stf = (ctypes.c_float * NSTAGES)()
+    if lib.ovh_stage_times(ctx.ptr, stf, NSTAGES) == NSTAGES:   # the last call's stages (HIP events)
+        out["samemsg4096_stage_ms"] = {lib.ovh_stage_name(k).decode(): round(float(stf[k]), 4) for k in range(NSTAGES)}
     # the same call with the same-message path off (OVH_SAMEMSG=0 at context creation): the
     # distinct-message batch path on the same votes
     os.environ["OVH_SAMEMSG"] = "0"
@@ -618,6 +626,9 @@ def main():
                 "vote_clock": clock,
                 "frac_of_fullrate_at_held_clock": (round(achieved * 1e12 / (256 * 64 * held * 1e9), 4)
                                                    if held else None),
+                "frac_of_1wave_chain_rate": round(achieved * 1e12 / PEAK_MAD_1WAVE_CHAIN, 4),
+                "one_wave_chain_basis": "v_mad_u64_u32 on one dependent chain at one wave per SIMD (the vote "
+                                        "kernel's occupancy and the product's order), 2.6448e13 lane-ops/s",
                 "work_M_per_unit": work_M,
                 "work_basis": "SURVEY 8(d) canonical W_v minus MSM + merge + amortised FE" if dname in canon
                               else "program heavy ops (workmodel.json)",

@@ -881,14 +881,14 @@ __global__ __launch_bounds__(64) void k_vm_g1pairs(uint32_t npairs, VmDev prog, 
 // Per distinct hash (one wave): f_g = Miller(apk_g, H_g) -> the group slab's f planes; apk_g =
 // P[head[g]] (its votes' r pk summed, the identity when none of them passed its checks or
 // H_g = O), and then f_g = 1 (e(O, H) = 1).
-__global__ __launch_bounds__(64) void k_vm_gmil(uint32_t G, VmDev prog, const uint32_t* __restrict__ cst_g,
+__global__ __launch_bounds__(64) void k_vm_gmil(uint32_t G, uint32_t q0, VmDev prog, const uint32_t* __restrict__ cst_g,
                                                 const uint32_t* __restrict__ head, Slab P, Slab g) {
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
   uint32_t* slots = lds + SLOT_BASE_W;
   __shared__ uint32_t zinf;
-  const uint32_t q = blockIdx.x, lane = threadIdx.x;
+  const uint32_t q = q0 + blockIdx.x, lane = threadIdx.x;
   if (q >= G) return;
   const uint32_t a = head[q];
   load_consts(cst, cst_g, VM_NCONST);
@@ -939,6 +939,55 @@ __global__ __launch_bounds__(64) void k_vm_vote1h_b(uint32_t cnt, uint32_t lo, V
     vote_wave<false, true>(prog, VM_VOTE1H_NPHASES, VM_VOTE1H_NSLOTS, VM_VOTE1H_IN, VM_VOTE1H_OUT, cst_g,
                            pks + (size_t)j * 48, pk, e, sigs + (size_t)j * 96, s, i, 1, codes + i, gH, gid[i],
                            ghinf + gid[i]);
+}
+
+// The combined check of a same-message batch (one wave): F (the Miller values of hashes 1..G-1,
+// folded to one; the identity when F.p is null) x Miller(apk_0, H_0) x Miller(-G1, S) as one
+// two-pair Miller loop, then FE == 1 -> *verdict (program gfin). apk_0 = P[head[0]], S = the
+// MSM's sum. When apk_0 or S is the identity (every vote of hash 0 failed, or no vote passed its
+// checks) the pair cannot enter the shared loop: the verdict is 0 and the per-vote bisection
+// decides every code exactly.
+static_assert(VM_GFIN_W == 64 && VM_GFIN_NIN == 27, "gfin inputs: F, apk, H, S");
+__global__ __launch_bounds__(64) void k_vm_gfin(VmDev prog, const uint32_t* __restrict__ cst_g, Slab F,
+                                                const uint32_t* __restrict__ head, Slab P, Slab gH, Slab S,
+                                                int32_t* __restrict__ verdict) {
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  uint32_t* cst = lds;
+  uint32_t* slots = lds + SLOT_BASE_W;
+  __shared__ uint32_t degenerate;
+  const uint32_t lane = threadIdx.x, a = head[0];
+  load_consts(cst, cst_g, VM_NCONST);
+  if (lane == 0) {
+    Fp za, zs;
+    P.ld(za, 2, a);
+    S.ld(zs, 4, 0);
+    Fp zs1;
+    S.ld(zs1, 5, 0);
+    degenerate = (fp_is_zero(za) || (fp_is_zero(zs) && fp_is_zero(zs1))) ? 1u : 0u;
+  }
+  if (lane < 27) {
+    Fp v;
+    if (lane < 12) {
+      if (F.p) F.ld(v, lane, 0);
+      else if (lane == 0) fp_one(v);
+      else fp_zero(v);
+    } else if (lane < 15) {
+      P.ld(v, lane - 12, a);
+    } else if (lane < 21) {
+      gH.ld(v, lane - 15, 0);
+    } else {
+      S.ld(v, lane - 21, 0);
+    }
+    slot_put(slots, VM_GFIN_IN[lane], v.v);
+  }
+  __syncthreads();
+  if (degenerate) {  // wave-uniform
+    if (lane == 0) *verdict = 0;
+    return;
+  }
+  vm::run(prog.code, VM_GFIN_NPHASES, 64, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0});
+  if (lane == 0) *verdict = slot_flag_get(slots, VM_GFIN_OUT[0]) ? 1 : 0;
 }
 
 // verify_aggregated_signature (verify_aggregated_vm), the part without the aggregated key, on a
@@ -1980,7 +2029,7 @@ struct ovh_ctx {
   // Fp-VM programs + constant table in device memory
   // same-message batches (verify_samemsg_locked): programs, per slot the group slab (G_PLANES
   // planes + the H-is-infinity words, gcap entries); OVH_SAMEMSG=0 turns the path off
-  VmDev vm_vsame{}, vm_vsame_t{}, vm_h2g{}, vm_gmil{}, vm_pkdec{}, vm_g1grp{};
+  VmDev vm_vsame{}, vm_vsame_t{}, vm_h2g{}, vm_gmil{}, vm_pkdec{}, vm_g1grp{}, vm_gfin{};
   uint32_t* gslab[OVH_BATCH_SLOTS] = {};
   uint32_t gcap[OVH_BATCH_SLOTS] = {};
   bool samemsg = true;
@@ -2067,6 +2116,8 @@ static constexpr size_t LDS_PKDEC = ((size_t)SLOT_BASE_W + (64 / VM_PKDEC_W) * (
 static_assert(LDS_PKDEC <= 64 * 1024 && VM_PKDEC_NIN == 2, "pkdec LDS / shape");
 static constexpr size_t LDS_G1GRP = ((size_t)SLOT_BASE_W + (size_t)G1GRP_STRIDE_W) * 4;
 static_assert(LDS_G1GRP <= 64 * 1024 && VM_G1GRP_NIN == 3, "g1grp LDS / shape");
+static constexpr size_t LDS_GFIN = ((size_t)SLOT_BASE_W + (size_t)VM_GFIN_NSLOTS * 12) * 4;
+static_assert(LDS_GFIN + 16 <= 64 * 1024, "gfin LDS");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
 // allocation granules assumed)
 constexpr size_t lds_granule(size_t b) { return (b + 1023) / 1024 * 1024; }
@@ -2159,6 +2210,8 @@ static int vm_init(ovh_ctx* c) {
                 VM_VSAME_T_NIN, VM_VSAME_T_OUT, VM_VSAME_T_NOUT));
   CHK(vm_upload(c, c->vm_h2g, VM_H2G_CODE, VM_H2G_NPHASES, VM_H2G_W, VM_H2G_NW, VM_H2G_IN, VM_H2G_NIN, VM_H2G_OUT,
                 VM_H2G_NOUT));
+  CHK(vm_upload(c, c->vm_gfin, VM_GFIN_CODE, VM_GFIN_NPHASES, VM_GFIN_W, VM_GFIN_NW, VM_GFIN_IN, VM_GFIN_NIN, VM_GFIN_OUT,
+                VM_GFIN_NOUT));
   CHK(vm_upload(c, c->vm_g1grp, VM_G1GRP_CODE, VM_G1GRP_NPHASES, VM_G1GRP_W, VM_G1GRP_NW, VM_G1GRP_IN, VM_G1GRP_NIN,
                 VM_G1GRP_OUT, VM_G1GRP_NOUT));
   CHK(vm_upload(c, c->vm_pkdec, VM_PKDEC_CODE, VM_PKDEC_NPHASES, VM_PKDEC_W, VM_PKDEC_NW, VM_PKDEC_IN, VM_PKDEC_NIN,
@@ -2895,17 +2948,25 @@ static int verify_samemsg_locked(ovh_ctx* c, size_t n, uint8_t* d, size_t t, con
       k_vm_g1pairs<<<(np + 64 / VM_G1PADD_W - 1) / (64 / VM_G1PADD_W), 64, LDS_G1PADD, xs>>>(
           np, c->vm_g1padd, G1PADD_STRIDE_W, c->vm_consts, pairs + 2 * (size_t)a, P);
     }
-    k_vm_gmil<<<G, 64, LDS_GMIL, xs>>>(G, c->vm_gmil, c->vm_consts, head, P, g);
-    k_vm_fold<VM_FOLD_UNITS><<<(m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, xs>>>(
-        G, c->vm_fold, c->vm_consts, Slab{g.p + (size_t)VM_G_F * 12 * g.cap, g.cap}, Slab{nullptr, 0},
-        region_F(c, slot, 0), nullptr);
+    // hashes 1..G-1: their own Miller loops, folded to one F; hash 0's pair joins the final's loop
+    if (G > 1) {
+      m = (G - 1 + 3) / 4;
+      k_vm_gmil<<<G - 1, 64, LDS_GMIL, xs>>>(G, 1, c->vm_gmil, c->vm_consts, head, P, g);
+      k_vm_fold<VM_FOLD_UNITS><<<(m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, xs>>>(
+          G - 1, c->vm_fold, c->vm_consts, Slab{g.p + (size_t)VM_G_F * 12 * g.cap + 1, g.cap}, Slab{nullptr, 0},
+          region_F(c, slot, 0), nullptr);
+    }
   }
-  CHK(fold_down(c, slot, xs, 1, &reg, &m, 4));
+  if (G > 1) CHK(fold_down(c, slot, xs, 1, &reg, &m, 1));
   CHK(enqueue_msm(c, fst, slot, N, dc));
   HIPCHK(hipEventRecord(c->ev_x[3], xs));
   HIPCHK(hipStreamWaitEvent(fst, c->ev_x[3], 0));
   int32_t* verdict = c->result + RES_BATCH + slot;
-  enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict, msm_S(c, slot));
+  {
+    StageScope p(c, ST_FINAL, fst);
+    k_vm_gfin<<<1, 64, LDS_GFIN, fst>>>(c->vm_gfin, c->vm_consts, G > 1 ? region_F(c, slot, reg) : Slab{nullptr, 0},
+                                        head, P, gH, msm_S(c, slot), verdict);
+  }
   {
     StageScope p(c, ST_FALLBACK, fst);
     const PkSrc tab{c->tab.planes, c->tab.cap, c->tab.flags, (int32_t*)(d + n * 180)};
@@ -3536,6 +3597,54 @@ void ovh_destroy(ovh_ctx* c) {
 }
 
 int ovh_device_count(ovh_ctx* c) { return !c ? 0 : c->sub.empty() ? 1 : (int)c->sub.size(); }
+
+// Diagnostics: occupancy A/B of a VM program. `prog` 0 = vsame (75 slots:
+// eight workgroups fit a CU's LDS), 1 = vote (159 slots: four); `reps` launches over n votes of
+// whatever the state slab holds (the programs are branch-free: the input values do not change
+// the work), all on the main stream (streams = 1: one launch after the other) or alternating over
+// the main and the side stream (streams = 2: two launches co-resident when the LDS allows: two
+// waves per SIMD). *ms = the wall time of the whole sequence (HIP events).
+int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams, float* ms) {
+  if (!c || !ms || n == 0 || n > (1u << 20) || reps < 1 || streams < 1 || streams > 2 || prog < 0 || prog > 1)
+    return OVH_ERR_ARG;
+  if (!c->sub.empty()) c = c->sub[0];
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  CHK(ensure_cap(c, n));
+  CHK(ensure_in(c, n * 176 + 64));
+  CHK(sync_all(c));
+  if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+  HIPCHK(hipMemsetAsync(c->in_buf, 0, n * 176, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const Slab s{c->state_slot[0], c->cap};
+  int32_t* dc = (int32_t*)(c->in_buf + n * 144);
+  const uint32_t N = (uint32_t)n;
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  HIPCHK(hipEventRecord(e0, c->stream));
+  HIPCHK(hipStreamWaitEvent(c->xstream, e0, 0));
+  for (int r = 0; r < reps; ++r) {
+    const hipStream_t st = (streams == 2 && (r & 1)) ? c->xstream : c->stream;
+    if (prog == 0)
+      k_vm_vsame<false><<<(N + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(N, 0, c->vm_vsame, c->vm_consts,
+                                                                               c->in_buf + n * 96, PkSrc{}, c->in_buf,
+                                                                               s, 1, 0, dc);
+    else
+      k_vm_vote<<<(N + VM_SLICES - 1) / VM_SLICES, 64, LDS_VOTE, st>>>(N, c->vm_vote, c->vm_fold, c->vm_consts,
+                                                                      c->in_buf + n * 96, c->in_buf, s, 1, 0, dc,
+                                                                      region_F(c, 0, 0), nullptr);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(e1, c->xstream));
+  HIPCHK(hipStreamWaitEvent(c->stream, e1, 0));
+  HIPCHK(hipEventRecord(e1, c->stream));
+  HIPCHK(hipEventSynchronize(e1));
+  HIPCHK(hipEventElapsedTime(ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return 0;
+}
 
 int ovh_vm_trace(ovh_ctx* c, int prog, uint64_t* stamps, size_t max) {
   if (!c || prog < 0 || prog > 3 || (max && !stamps)) return -OVH_ERR_ARG;

@@ -245,6 +245,10 @@ const char* ovh_stage_name(int stage);
  * read after each phase barrier: copies min(max, nphases + 1) stamps, returns nphases + 1
  * (0 without the flag, <0 on error). */
 int ovh_vm_trace(ovh_ctx* ctx, int prog, uint64_t* stamps, size_t max);
+/* Diagnostics: occupancy A/B of a VM program -- `reps` launches of program `prog` (0 vsame, 1
+ * vote) over n votes, on one stream (streams = 1) or alternating over two (streams = 2: two
+ * launches co-resident when the LDS allows, i.e. two waves per SIMD). *ms = wall time. */
+int ovh_diag_vm_occupancy(ovh_ctx* ctx, int prog, size_t n, int reps, int streams, float* ms);
 /* Diagnostics (context created with OVH_FLAG_VM_CLOCK): per workgroup of the last vote / vote_t
  * launch, (delta s_memtime, delta s_memrealtime) around its VM program -- shader cycles and
  * 100 MHz ticks, so the clock the kernel held is delta_memtime / delta_realtime x 100 MHz

@@ -121,6 +121,11 @@ def test_hash_whose_every_vote_fails_and_all_valid_batches():
     assert want[:40].tolist() == [0] * 40 and want[40:].tolist() == [5] * 24
     got = cc.verify_batch(list(map(bytes, sigs)), list(map(bytes, hs)), list(map(bytes, pks)))
     assert got.tolist() == want.tolist()
+    # the failing hash first: its pair cannot join the final's loop (k_vm_gfin: verdict 0), the
+    # per-vote bisection decides
+    rev = np.concatenate([np.arange(40, 64), np.arange(40)])
+    got = cc.verify_batch(list(map(bytes, sigs[rev])), list(map(bytes, hs[rev])), list(map(bytes, pks[rev])))
+    assert got.tolist() == want[rev].tolist()
     got = cc.verify_batch(list(map(bytes, sa)), [da] * 40, list(map(bytes, pa)))
     assert got.tolist() == [0] * 40
     # one vote per hash on average is not a same-message batch

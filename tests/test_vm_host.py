@@ -283,3 +283,8 @@ def test_samemsg_programs_on_interpreter(hx, built, golden_votes, any_all):  # n
     o = run("vsame", {n: inp[n] for n in progs.VSAME_IN}, r)
     mi = dict(zip(progs.GMIL_IN, [o["st:r%d" % j] for j in range(3)] + [h["st:h%d" % j] for j in range(6)]))
     run("gmil", mi)
+    sig = bls.g2_from_bytes(bytes.fromhex(g["votes"][0]["sig"]))
+    rs = bls.pt_mul(bls.Fp2Ops, sig, gen.alg.rlc_scalar(r))
+    fin = dict(zip(progs.GFIN_IN, [1] + [0] * 11 + [o["st:r%d" % j] for j in range(3)] +
+                   [h["st:h%d" % j] for j in range(6)] + gen._proj(rs)))
+    assert run("gfin", fin) == {"ok": 1}

@@ -35,13 +35,13 @@ WIDTH.update({"sigchk": 16, "pkchk": 16, "g1padd": 8, "vote1": 64, "vote_t1": 64
               "final1": 64})
 # same-message batches (r04): per vote a 16-lane slice, per distinct hash one 16-lane slice for
 # hash_to_G2 and one wave for its Miller loop (the latency of a round's group)
-WIDTH.update({"vsame": 16, "vsame_t": 16, "h2g": 16, "gmil": 64, "pkdec": 4, "g1grp": 16})
-MAX_SLOTS = {"vsame": 400, "vsame_t": 400, "h2g": 400, "gmil": 1200, "vote": 200, "vote_t": 200, "fold": 256, "final": 2048, "final1": 2048, "vote1": 1200, "vote_t1": 1200,
+WIDTH.update({"vsame": 16, "vsame_t": 16, "h2g": 16, "gmil": 64, "pkdec": 4, "g1grp": 16, "gfin": 64})
+MAX_SLOTS = {"gfin": 2048, "vsame": 400, "vsame_t": 400, "h2g": 400, "gmil": 1200, "vote": 200, "vote_t": 200, "fold": 256, "final": 2048, "final1": 2048, "vote1": 1200, "vote_t1": 1200,
              "votew": 1200, "votew_t": 1200, "qcpre": 1200, "qcmil": 1200, "vote1h": 1200, "vote_t1h": 1200}
 # phases an op may run ahead of its first consumer's earliest start (sched.schedule `hoist`)
-HOIST = {"vsame": 250, "vsame_t": 250, "h2g": 250, "gmil": 250, "vote": 250, "vote_t": 250, "final": 50, "vote1": 250, "vote_t1": 250, "final1": 50, "votew": 250,
+HOIST = {"gfin": 50, "vsame": 250, "vsame_t": 250, "h2g": 250, "gmil": 250, "vote": 250, "vote_t": 250, "final": 50, "vote1": 250, "vote_t1": 250, "final1": 50, "votew": 250,
          "votew_t": 250, "qcpre": 250, "qcmil": 250, "vote1h": 250, "vote_t1h": 250}
-STRETCH = {"vsame": 1.0, "vsame_t": 1.0, "h2g": 1.0, "gmil": 1.0, "final": 1.0, "vote": 1.0, "vote_t": 1.0, "vote1": 1.0, "vote_t1": 1.0, "final1": 1.0, "votew": 1.0,
+STRETCH = {"gfin": 1.0, "vsame": 1.0, "vsame_t": 1.0, "h2g": 1.0, "gmil": 1.0, "final": 1.0, "vote": 1.0, "vote_t": 1.0, "vote1": 1.0, "vote_t1": 1.0, "final1": 1.0, "votew": 1.0,
            "votew_t": 1.0, "qcpre": 1.0, "qcmil": 1.0, "vote1h": 1.0, "vote_t1h": 1.0}
 # priority weight of a heavy op against a light one (path length in weighted ops). r03 scan on
 # the cost model (product phase 1.60 us, linear 0.69 us): vote 4 -> 64 estimates 3.29 -> 3.10 ms
@@ -311,6 +311,15 @@ def check_samemsg(built, bls, g):
         f = progs.unflat12([mgot["st:f%d" % j] for j in range(12)])
         assert bls.f12_eq(bls.final_exponentiation_x_chain(f),
                           bls.final_exponentiation_x_chain(bls.miller_loop(rP, bls.hash_to_g2(h)))), "gmil: f"
+        # gfin: F = 1, apk_0 = r pk, H_0, S = r sigma -> ok; S from another scalar -> not ok
+        fprog, fsc, fwords, fins, _ = built["gfin"]
+        rs = bls.pt_mul(bls.Fp2Ops, sig, alg.rlc_scalar(r))
+        one12 = [1] + [0] * 11
+        for S_, want in ((rs, 1), (bls.pt_mul(bls.Fp2Ops, sig, alg.rlc_scalar(r) + 1), 0)):
+            finp = dict(zip(fins, one12 + [X, Y, Z] + Hp + _proj(S_)))
+            assert fprog.evaluate(finp)[fprog.outputs["ok"]] == want, "gfin"
+            if want:
+                assert sched.simulate(fsc, fwords, finp) == {"ok": 1}, "gfin: simulated"
     dprog, dsc, dwords, dins, _ = built["pkdec"]
     named = {c["name"]: bytes.fromhex(c["pk"]) for c in g["verify"]}
     for pkb, ok in [(bytes.fromhex(k["pk"]), 1) for k in g["keys"][:2]] + [(named["pk_not_on_curve"], 0)]:

@@ -707,6 +707,26 @@ def build_gmil():
 
 PROGRAMS["pkdec"] = (build_pkdec, PKCHK_IN, PKDEC_OUT)
 PROGRAMS["g1grp"] = (build_g1grp, G1GRP_IN, G1GRP_OUT)
+GFIN_IN = f12_names("F") + ["pk_X", "pk_Y", "pk_Z"] + g2p_names("h") + g2p_names("S")
+
+
+def build_gfin():
+    """The combined check of a same-message batch: F (the other hashes' Miller values, folded) x
+    Miller(apk_0, H_0) x Miller(-G1, S) as one two-pair Miller loop, then the final
+    exponentiation == 1 (apk_0 and S not the identity: the kernel decides otherwise)."""
+    p = Prog("gfin")
+    a = Alg(p, inv_op=True, use_sop=USE_SOP)
+    F = unflat12([p.input(n) for n in f12_names("F")])
+    P0 = (p.input("pk_X"), p.input("pk_Y"), p.input("pk_Z"))
+    H = unflat_g2p([p.input(n) for n in g2p_names("h")])
+    S = unflat_g2p([p.input(n) for n in g2p_names("S")])
+    ng1 = (p.const(G1X), p.const(-G1Y))
+    m = a.miller_loop_multi([(P0, H), (ng1, S)])
+    p.output("ok", a.f12_eq_one(a.final_exp(a.f12_mul(F, m))))
+    return p
+
+
+PROGRAMS["gfin"] = (build_gfin, GFIN_IN, ["ok"])
 PROGRAMS["vsame"] = (build_vsame(False), VSAME_IN, VSAME_OUT)
 PROGRAMS["vsame_t"] = (build_vsame(True), VSAME_T_IN, VSAME_T_OUT)
 PROGRAMS["h2g"] = (build_h2g, H2G_IN, H2G_OUT)

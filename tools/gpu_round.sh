@@ -21,5 +21,5 @@ if [ -n "${Q8:-}" ]; then
   GPU_MAX_HW_QUEUES=8 timeout -k 10 200 python -u bench.py --steps ${STEPS:-30} --warmup 2 --no-cpu-baseline --no-latency --shard-path > "$OUT/bench_shard_q8.log" 2>&1
 fi
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$R/bench.py" --steps ${STEPS:-30} --warmup 2 --no-cpu-baseline > "$OUT/bench_prof.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- python3 "$R/bench.py" --steps ${STEPS:-30} --warmup 2 --no-cpu-baseline --no-latency --clock-seconds 0 > "$OUT/bench_prof.log" 2>&1
 echo done > "$OUT/ok"

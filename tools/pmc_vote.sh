@@ -8,7 +8,7 @@ OUT=$R/gpurun_out/${TAG:-pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-B="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-latency"
+B="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-latency --clock-seconds 0"
 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY \
   SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/a" -o a --output-format csv -- $B > "$OUT/a.log" 2>&1
 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_MISC \
