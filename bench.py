@@ -166,8 +166,9 @@ def latencies(ctx, sigs, hs, pks) -> dict:
                      path: one hash_to_G2 + one Miller loop for the batch), median of 3
       round99_ms     the ingress shim (ingress.VoteIngress at proc_network_msg) on a relayer of a
                      100-validator round: 99 SignedVote messages in, decode + device vote digests
-                     + one same-message prefetch, the N-1 trigger flushing them to overlord;
-                     median of 3 rounds"""
+                     + one prefetch (default routing: the small-batch path at 99 votes), the N-1
+                     trigger flushing them to overlord; median of 3 rounds; round99_samemsg_ms
+                     the same with the same-message path forced (OVH_SAMEMSG=2)"""
     import torch
     from consensus_overlord_amd import device as dev
     lib = ctx.lib
@@ -306,6 +307,25 @@ def samemsg_probes(ctx, pks) -> dict:
     stf = (ctypes.c_float * NSTAGES)()
     if lib.ovh_stage_times(ctx.ptr, stf, NSTAGES) == NSTAGES:   # the last call's stages (HIP events)
         out["samemsg4096_stage_ms"] = {lib.ovh_stage_name(k).decode(): round(float(stf[k]), 4) for k in range(NSTAGES)}
+    # pipelined: batches of the same votes in device memory through ovh_verify_samemsg_device_async
+    # (OVH_BATCH_SLOTS in flight, one codes buffer per batch), timed from the first enqueue to
+    # ovh_batch_wait -- the same-message counterpart of the headline value
+    kb = 24
+    sg_d, pk_d = torch.from_numpy(sg).cuda(), pks.contiguous()
+    cd = torch.full((kb, n), -1, dtype=torch.int32, device="cuda")
+    for j in range(3):
+        dev.verify_samemsg_async(ctx, sg_d, digest, pk_d, cd[j])
+    dev.batch_wait(ctx)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for j in range(kb):
+        dev.verify_samemsg_async(ctx, sg_d, digest, pk_d, cd[j])
+    dev.batch_wait(ctx)
+    el = time.perf_counter() - t
+    if (cd != 0).any():
+        raise RuntimeError("pipelined same-message batches: rejected votes")
+    out["samemsg4096_pipelined_ms_per_batch"] = round(el / kb * 1e3, 3)
+    out["samemsg4096_pipelined_verifs_per_s"] = round(kb * n / el, 1)
     # the same call with the same-message path off (OVH_SAMEMSG=0 at context creation): the
     # distinct-message batch path on the same votes
     os.environ["OVH_SAMEMSG"] = "0"
@@ -329,10 +349,10 @@ def samemsg_probes(ctx, pks) -> dict:
     vpk = dev.sk_to_pk_batch(ctx, vs).cpu().numpy()
     rts, rts_off = [], []
     for rnd in range(8):
-        if rnd in (0, 4):   # rounds 0-3: the same-message path; 4-7: OVH_SAMEMSG=0 (the small-batch path)
-            if rnd:
+        if rnd in (0, 4):   # rounds 0-3: the default routing (99 votes: the small-batch path);
+            if rnd:         # rounds 4-7: OVH_SAMEMSG=2 (the same-message path at any size)
                 node.ctx.close()
-                os.environ["OVH_SAMEMSG"] = "0"
+                os.environ["OVH_SAMEMSG"] = "2"
             try:
                 node = ConsensusCrypto(bytes(sks_h[0]), ctx=Context(torch.cuda.current_device(), flags=FLAG_SK_RAW))
             finally:
@@ -359,7 +379,7 @@ def samemsg_probes(ctx, pks) -> dict:
         if rnd % 4:
             (rts if rnd < 4 else rts_off).append(dt)
     out["round99_ms"] = round(float(np.median(rts)) * 1e3, 3)
-    out["round99_off_ms"] = round(float(np.median(rts_off)) * 1e3, 3)
+    out["round99_samemsg_ms"] = round(float(np.median(rts_off)) * 1e3, 3)
     node.ctx.close()
     return out
 

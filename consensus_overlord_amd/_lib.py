@@ -46,6 +46,7 @@ SIGNATURES = [
     ("ovh_combine_partials_device", ctypes.c_int, [_vp, _sz, _vp, ctypes.POINTER(ctypes.c_int32)]),
     ("ovh_batch_fallback_device", ctypes.c_int, [_vp, _sz, _vp]),
     ("ovh_verify_batch_device_async", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp]),
+    ("ovh_verify_samemsg_device_async", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp]),
     ("ovh_verify_batch_async", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp]),
     ("ovh_batch_wait", ctypes.c_int, [_vp]),
     ("ovh_combine_partials_device_async", ctypes.c_int, [_vp, _sz, _vp, _sz, _vp, _vp]),

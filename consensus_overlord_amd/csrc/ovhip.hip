@@ -1963,6 +1963,8 @@ struct ovh_ctx {
   // SIMD with a vote wave and takes longer than a vote kernel there).
   hipStream_t fstream = nullptr, fstream2 = nullptr;
   hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse; lazy)
+  hipStream_t hstream[OVH_BATCH_SLOTS] = {};  // a same-message batch's hash_to_G2, per slot (lazy)
+  hipStream_t vstream[2] = {};  // ovh_verify_samemsg_device_async's per-vote streams, in turn (lazy)
   hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
@@ -2032,8 +2034,16 @@ struct ovh_ctx {
   VmDev vm_vsame{}, vm_vsame_t{}, vm_h2g{}, vm_gmil{}, vm_pkdec{}, vm_g1grp{}, vm_gfin{};
   uint32_t* gslab[OVH_BATCH_SLOTS] = {};
   uint32_t gcap[OVH_BATCH_SLOTS] = {};
-  bool samemsg = true;
+  // 0: off; 1 (default): batches above small_max votes (below it the small-batch path has the
+  // lower latency); 2: every batch with at most n / 2 distinct hashes
+  int samemsg = 1;
   uint64_t sm_batches = 0, sm_votes = 0, sm_hashes = 0;
+  // ovh_verify_samemsg_device_async: the one-hash plan of sm1_n votes (gid = 0 | head 0 | pairs)
+  // and its level offsets; the hash of each slot (32 B per slot)
+  uint32_t* sm1_plan = nullptr;
+  size_t sm1_n = 0;
+  std::vector<uint32_t> sm1_lo;
+  uint8_t* sm1_hash = nullptr;
   VmDev vm_vote{}, vm_vote_t{}, vm_fold{}, vm_final{}, vm_rs{}, vm_madd{}, vm_padd{}, vm_hdbl[5]{}, vm_sigchk{},
       vm_pkchk{}, vm_g1padd{}, vm_vote1{}, vm_vote_t1{}, vm_final1{}, vm_votew{},
       vm_votew_t{}, vm_qcpre{}, vm_qcmil{}, vm_vote1h{}, vm_vote_t1h{}, vm_pkgen{}, vm_signg0{}, vm_signg1{};
@@ -2484,9 +2494,10 @@ static int fold_down(ovh_ctx* c, int slot, hipStream_t st, int slices, int* reg,
 
 // Verdict words in c->result: [0] single calls, then per slot the batch verdicts, the combine
 // verdicts, then the synchronous combine's and the multi-device combine's.
+enum { RES_WORDS = 32 };
 enum { RES_BATCH = 4, RES_COMBINE = RES_BATCH + OVH_BATCH_SLOTS, RES_SYNC = RES_COMBINE + OVH_BATCH_SLOTS, RES_MULTI };
 // RES_MULTI: the synchronous multi-device verdict; RES_MULTI + 1 + ring slot: the pipelined ones
-static_assert(RES_MULTI + 1 + OVH_BATCH_SLOTS <= 16, "verdict words fit c->result");
+static_assert(RES_MULTI + 1 + OVH_BATCH_SLOTS <= RES_WORDS, "verdict words fit c->result");
 
 // Final check on <= 4 partials given as planes: k_vm_final on stream `st`, verdict to *d_res;
 // xS: the batch's MSM result (partial 0's S), or {nullptr} when the partials carry their S.
@@ -2880,16 +2891,39 @@ static void samemsg_plan(size_t n, const uint8_t* hashes, const std::vector<uint
   pl.bytes = 4 * n + 32 * (size_t)pl.G + 4 * (size_t)pl.G + 4 * pl.pairs.size();
 }
 
-// The batch's state is staged at d (stage_split layout: sigs | hashes | pks | codes | table
-// indices; table votes [0, t)); the plan's arrays at d + pl.off. Main stream: the per-vote
-// programs (vsame_t over the table votes, vsame over the others); the slot's final stream, beside
-// them: hash_to_field + hash_to_G2 per distinct hash; then (final stream) the H = O codes, the
-// per-hash sums of r pk, the per-hash Miller loops, their fold, the MSM of sum r_i sigma_i, the
-// final check, and -- gated on its verdict -- the per-vote bisection. Caller holds c->mu.
-static int verify_samemsg_locked(ovh_ctx* c, size_t n, uint8_t* d, size_t t, const SameMsgPlan& pl, int32_t* dc) {
-  CHK(ensure_cap(c, n));
-  int slot;
-  CHK(take_slot(c, &slot));
+// A same-message batch in `slot` (taken by the caller): sigs (n x 96), the table votes [0, t)
+// with their table indices tidx, the other votes' keys pks (n - t x 48); the plan's device arrays
+// gid | ghash | head | pairs (SameMsgPlan) and its host level offsets. Main stream: the per-vote
+// programs (vsame_t over the table votes, vsame over the others); the side stream, beside them:
+// hash_to_field + hash_to_G2 per distinct hash; then (final stream) the H = O codes, (side stream)
+// the per-hash sums of r pk, the per-hash Miller loops and their fold, beside (final stream) the
+// MSM of sum r_i sigma_i, the final check, and -- gated on its verdict -- the per-vote bisection.
+// Nothing waits on the host: ovh_verify_batch syncs, ovh_verify_samemsg_device_async does not.
+// one (that API: a single hash, as a kernel argument): vsame runs on one of two per-vote streams
+// in turn, so consecutive batches' vsame grids are co-resident (two waves per SIMD: 1.36x the
+// throughput of one, profiles/r04e_occupancy_ab.json), and the hash goes to the slot's hash
+// stream without waiting for the per-vote work. Caller holds c->mu and has called
+// ensure_cap(c, n).
+// The 32-byte hash of a one-hash batch into its slot's device word (a kernel argument, so the
+// host's copy may change as soon as the launch returns).
+struct Hash32 {
+  uint32_t w[8];
+};
+__global__ void k_put_hash(Hash32 h, uint8_t* dst) {
+  if (threadIdx.x < 8) reinterpret_cast<uint32_t*>(dst)[threadIdx.x] = h.w[threadIdx.x];
+}
+
+struct SameMsgDev {
+  uint32_t G;
+  const uint32_t* gid;
+  const uint8_t* ghash;
+  const uint32_t* head;
+  const uint32_t* pairs;
+  const std::vector<uint32_t>* level_off;
+};
+
+static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* sigs, size_t t, const int32_t* tidx,
+                                 const uint8_t* pks, const SameMsgDev& pl, int32_t* dc, const Hash32* one = nullptr) {
   if (!c->gslab[slot] || c->gcap[slot] < c->cap) {
     if (c->gslab[slot]) (void)hipFree(c->gslab[slot]);
     c->gslab[slot] = nullptr;
@@ -2902,34 +2936,50 @@ static int verify_samemsg_locked(ovh_ctx* c, size_t n, uint8_t* d, size_t t, con
   const Slab gH{g.p + (size_t)VM_G_H * 12 * g.cap, g.cap};
   const Slab s{c->state_slot[slot], c->cap};
   const Slab P{s.p + (size_t)S_F * 12 * s.cap, s.cap};  // r pk of every vote, then the sums in place
-  const uint8_t* ex = d + pl.off;
-  const uint32_t* gid = (const uint32_t*)ex;
-  const uint8_t* ghash = ex + 4 * n;
-  const uint32_t* head = (const uint32_t*)(ghash + 32 * (size_t)G);
-  const uint32_t* pairs = head + G;
+  const uint32_t* gid = pl.gid;
+  const uint8_t* ghash = pl.ghash;
+  const uint32_t* head = pl.head;
+  const uint32_t* pairs = pl.pairs;
   c->ev_mask = 0;
   uint64_t seed, base;
   CHK(draw_seed(c, &seed, &base));
   c->slot_seed[slot] = seed;
   c->slot_base[slot] = base;
-  const hipStream_t st = c->stream, fst = c->fs[slot];
-  HIPCHK(hipEventRecord(c->ev_front[slot], st));  // the staged inputs
-  HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
-  {
-    StageScope p(c, ST_H2F, fst);
-    k_h2f<<<nblk(G), WG, 0, fst>>>(G, ghash, c->xmd, g);
-    k_vm_h2g<<<(G + VM_SLICES - 1) / VM_SLICES, 64, LDS_H2G, fst>>>(G, c->vm_h2g, c->vm_consts, g, ghinf);
+  const hipStream_t fst = c->fs[slot];
+  hipStream_t st = c->stream;
+  if (one) {
+    hipStream_t& v = c->vstream[c->pipe_k & 1];
+    if (!v) HIPCHK(hipStreamCreateWithFlags(&v, hipStreamNonBlocking));
+    st = v;
   }
+  // hash_to_G2 per hash on the slot's own stream (normal priority, beside the per-vote programs:
+  // at the final streams' low priority it took 2.8 ms beside 1,024 vsame waves, r04g; one stream
+  // per slot, so pipelined batches' hash_to_G2 chains overlap instead of queueing behind each
+  // other and the key sums)
+  if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+  if (!c->hstream[slot]) HIPCHK(hipStreamCreateWithFlags(&c->hstream[slot], hipStreamNonBlocking));
+  const hipStream_t xs = c->xstream, hs = c->hstream[slot];
+  HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));  // the inputs (and the slot free: take_slot)
+  HIPCHK(hipStreamWaitEvent(hs, c->ev_front[slot], 0));
+  HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
+  if (st != c->stream) HIPCHK(hipStreamWaitEvent(st, c->ev_front[slot], 0));
+  {
+    StageScope p(c, ST_H2F, hs);
+    if (one) k_put_hash<<<1, 64, 0, hs>>>(*one, (uint8_t*)ghash);
+    k_h2f<<<nblk(G), WG, 0, hs>>>(G, ghash, c->xmd, g);
+    k_vm_h2g<<<(G + VM_SLICES - 1) / VM_SLICES, 64, LDS_H2G, hs>>>(G, c->vm_h2g, c->vm_consts, g, ghinf);
+  }
+  HIPCHK(hipEventRecord(c->ev_x[1], hs));
+  HIPCHK(hipStreamWaitEvent(fst, c->ev_x[1], 0));
+  const PkSrc tab{c->tab.planes, c->tab.cap, c->tab.flags, tidx};
   {
     StageScope p(c, ST_VOTE, st);
-    const PkSrc tab{c->tab.planes, c->tab.cap, c->tab.flags, (int32_t*)(d + n * 180)};
     if (T)
       k_vm_vsame<true><<<(T + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(T, 0, c->vm_vsame_t, c->vm_consts, nullptr,
-                                                                              tab, d, s, seed, base, dc);
+                                                                              tab, sigs, s, seed, base, dc);
     if (N > T)
       k_vm_vsame<false><<<(N - T + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(
-          N - T, T, c->vm_vsame, c->vm_consts, d + n * 128 + 48 * (size_t)T, PkSrc{}, d + 96 * (size_t)T, s, seed, base,
-          dc);
+          N - T, T, c->vm_vsame, c->vm_consts, pks, PkSrc{}, sigs + 96 * (size_t)T, s, seed, base, dc);
   }
   HIPCHK(hipEventRecord(c->ev_front[slot], st));
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
@@ -2937,14 +2987,13 @@ static int verify_samemsg_locked(ovh_ctx* c, size_t n, uint8_t* d, size_t t, con
   uint32_t m = (G + 3) / 4;
   k_samemsg_fix<<<nblk(n), WG, 0, fst>>>(N, gid, ghinf, dc, P);
   // the per-hash key sums, Miller loops and their fold on the side stream, beside the MSM
-  if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-  const hipStream_t xs = c->xstream;
   HIPCHK(hipEventRecord(c->ev_x[2], fst));
   HIPCHK(hipStreamWaitEvent(xs, c->ev_x[2], 0));
   {
     StageScope p(c, ST_FOLD, xs);
-    for (size_t l = 0; l + 1 < pl.level_off.size(); ++l) {
-      const uint32_t a = pl.level_off[l], np = pl.level_off[l + 1] - a;
+    const std::vector<uint32_t>& lo = *pl.level_off;
+    for (size_t l = 0; l + 1 < lo.size(); ++l) {
+      const uint32_t a = lo[l], np = lo[l + 1] - a;
       k_vm_g1pairs<<<(np + 64 / VM_G1PADD_W - 1) / (64 / VM_G1PADD_W), 64, LDS_G1PADD, xs>>>(
           np, c->vm_g1padd, G1PADD_STRIDE_W, c->vm_consts, pairs + 2 * (size_t)a, P);
     }
@@ -2969,14 +3018,12 @@ static int verify_samemsg_locked(ovh_ctx* c, size_t n, uint8_t* d, size_t t, con
   }
   {
     StageScope p(c, ST_FALLBACK, fst);
-    const PkSrc tab{c->tab.planes, c->tab.cap, c->tab.flags, (int32_t*)(d + n * 180)};
     if (T)
-      k_vm_vote1h_b<true><<<T, 64, LDS_VOTE1H, fst>>>(T, 0, c->vm_vote_t1h, c->vm_consts, nullptr, tab, d, s, dc, gid,
+      k_vm_vote1h_b<true><<<T, 64, LDS_VOTE1H, fst>>>(T, 0, c->vm_vote_t1h, c->vm_consts, nullptr, tab, sigs, s, dc, gid,
                                                       gH, ghinf, verdict);
     if (N > T)
-      k_vm_vote1h_b<false><<<N - T, 64, LDS_VOTE1H, fst>>>(N - T, T, c->vm_vote1h, c->vm_consts,
-                                                           d + n * 128 + 48 * (size_t)T, PkSrc{}, d + 96 * (size_t)T, s,
-                                                           dc, gid, gH, ghinf, verdict);
+      k_vm_vote1h_b<false><<<N - T, 64, LDS_VOTE1H, fst>>>(N - T, T, c->vm_vote1h, c->vm_consts, pks, PkSrc{},
+                                                           sigs + 96 * (size_t)T, s, dc, gid, gH, ghinf, verdict);
     k_vm_votefe<<<N, 64, LDS_FINAL1, fst>>>(N, c->vm_final1, c->vm_consts, s, dc, verdict);
   }
   HIPCHK(hipEventRecord(c->ev_back[slot], fst));
@@ -3001,7 +3048,7 @@ static int verify_host_locked(ovh_ctx* c, size_t n, const uint8_t* sigs, const u
   const size_t t0 = table_split(c, n, pks, perm, tidx);
   (void)t0;
   bool same = false;
-  if (c->samemsg && n >= 2) {
+  if (n >= 2 && (c->samemsg >= 2 || (c->samemsg == 1 && n > c->small_max))) {
     samemsg_plan(n, hashes, perm, pl);
     same = 2 * (size_t)pl.G <= n;
   }
@@ -3019,7 +3066,13 @@ static int verify_host_locked(ovh_ctx* c, size_t n, const uint8_t* sigs, const u
     if (!pl.pairs.empty()) memcpy(h.data() + 4 * n + 36 * (size_t)pl.G, pl.pairs.data(), 4 * pl.pairs.size());
     HIPCHK(hipMemcpyAsync(d + pl.off, h.data(), pl.bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));  // the pageable copy of h completed before h dies
-    CHK(verify_samemsg_locked(c, n, d, t, pl, dc));
+    const uint8_t* ex = d + pl.off;
+    const uint32_t* head = (const uint32_t*)(ex + 4 * n + 32 * (size_t)pl.G);
+    const SameMsgDev pd{pl.G, (const uint32_t*)ex, ex + 4 * n, head, head + pl.G, &pl.level_off};
+    CHK(ensure_cap(c, n));
+    int slot;
+    CHK(take_slot(c, &slot));
+    CHK(verify_samemsg_locked(c, slot, n, d, t, (const int32_t*)(d + n * 180), d + n * 128 + 48 * t, pd, dc));
   } else if (n == 1) {
     CHK(verify_one_locked(c, d, d + 96, staged_key(c, n, d, t, 0), dc, hashes));
   } else {
@@ -3451,7 +3504,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   c->flags = flags;
   if (const char* e = getenv("OVH_FOLD_SIDE")) c->fold_side = atoi(e) != 0;
   if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
-  if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e) != 0;
+  if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e);
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->wg_cap = 4u * (uint32_t)ncu;
@@ -3465,9 +3518,9 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, 64) == hipSuccess &&
+            hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&
             hipMalloc(&c->vstart, 8) == hipSuccess && hipMemset(c->vstart, 0, 8) == hipSuccess &&
-            hipMemset(c->result, 0, 64) == hipSuccess &&
+            hipMemset(c->result, 0, RES_WORDS * 4) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
   // two finals in flight at most (LDS budget below: four vote workgroups and two finals fit a
   // CU; r02i ran one final stream per slot and lost 2.4 ms in every third vote kernel to a
@@ -3555,7 +3608,9 @@ int ovh_multi_peer_matrix(ovh_ctx* c, uint8_t* out, size_t cap) {
 static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1]})
+    if (s) (void)hipStreamSynchronize(s);
+  for (hipStream_t s : c->hstream)
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
@@ -3564,7 +3619,7 @@ static void destroy_one(ovh_ctx* c) {
   for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vstart, (void*)c->vm_consts,
                   (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
                   (void*)c->tab.planes, (void*)c->tab.flags, (void*)c->qc_buf, (void*)c->qt_buf, (void*)c->hc_planes, (void*)c->hc_inf, (void*)c->gather,
-                  (void*)c->mfin})
+                  (void*)c->mfin, (void*)c->sm1_plan, (void*)c->sm1_hash})
     if (p) (void)hipFree(p);
   for (void* p : c->vm_bufs) (void)hipFree(p);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
@@ -3584,7 +3639,9 @@ static void destroy_one(ovh_ctx* c) {
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1]})
+    if (s) (void)hipStreamDestroy(s);
+  for (hipStream_t s : c->hstream)
     if (s) (void)hipStreamDestroy(s);
   delete c;
 }
@@ -4499,6 +4556,38 @@ int ovh_verify_batch_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, c
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   return verify_async_locked(c, n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, true);
+}
+
+int ovh_verify_samemsg_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* hash,
+                                    const uint8_t* d_pks, int32_t* d_codes) {
+  if (!c || !c->sub.empty() || (n && (!d_sigs || !hash || !d_pks || !d_codes))) return OVH_ERR_ARG;
+  if (n == 0) return 0;
+  if (n > (1u << 24)) return OVH_ERR_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  CHK(ensure_cap(c, n));
+  if (n != c->sm1_n) {  // the plan of one group of n votes; batches in flight may read the old one
+    CHK(sync_all(c));
+    if (c->sm1_plan) (void)hipFree(c->sm1_plan);
+    c->sm1_plan = nullptr;
+    c->sm1_n = 0;
+    SameMsgPlan pl;
+    std::vector<uint8_t> one(32 * n, 0);
+    samemsg_plan(n, one.data(), {}, pl);
+    std::vector<uint32_t> h(n + 1 + pl.pairs.size(), 0);
+    std::copy(pl.pairs.begin(), pl.pairs.end(), h.begin() + n + 1);
+    HIPCHK(hipMalloc(&c->sm1_plan, h.size() * 4));
+    HIPCHK(hipMemcpy(c->sm1_plan, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    if (!c->sm1_hash) HIPCHK(hipMalloc(&c->sm1_hash, 32 * OVH_BATCH_SLOTS));
+    c->sm1_lo = pl.level_off;
+    c->sm1_n = n;
+  }
+  int slot;
+  CHK(take_slot(c, &slot));
+  Hash32 hv;
+  memcpy(hv.w, hash, 32);
+  const SameMsgDev pd{1, c->sm1_plan, c->sm1_hash + 32 * slot, c->sm1_plan + n, c->sm1_plan + n + 1, &c->sm1_lo};
+  return verify_samemsg_locked(c, slot, n, d_sigs, 0, nullptr, d_pks, pd, d_codes, &hv);
 }
 
 // every device's lock, root first (the multi-device entry points)

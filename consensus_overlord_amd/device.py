@@ -78,6 +78,16 @@ def verify_batch_async(ctx: Context, sigs: torch.Tensor, hashes: torch.Tensor, p
     raise_for(ctx.lib.ovh_verify_batch_device_async(ctx.ptr, n, _ptr(sigs), _ptr(hashes), _ptr(pks), _ptr(codes)))
 
 
+def verify_samemsg_async(ctx: Context, sigs: torch.Tensor, digest: bytes, pks: torch.Tensor,
+                         codes: torch.Tensor) -> None:
+    """Enqueue one batch of votes that all sign `digest` (ovh_verify_samemsg_device_async);
+    `codes` is final after batch_wait."""
+    if len(digest) != 32:
+        raise ValueError("digest must be 32 bytes")
+    n = sigs.shape[0]
+    raise_for(ctx.lib.ovh_verify_samemsg_device_async(ctx.ptr, n, _ptr(sigs), digest, _ptr(pks), _ptr(codes)))
+
+
 def combine_partials_async(ctx: Context, partials: torch.Tensor, n: int, codes: torch.Tensor, stream=None) -> None:
     """Enqueue the combined check of the gathered partials (stream-ordered after the gather on
     `stream`) and, device-gated on its verdict, the bisection of this rank's last partial's n

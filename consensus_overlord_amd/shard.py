@@ -26,7 +26,7 @@ import torch
 import torch.distributed as dist
 
 PARTIAL_BYTES = 864
-BATCH_SLOTS = 3      # include/ovhip.h OVH_BATCH_SLOTS: batches in flight per context
+BATCH_SLOTS = 6      # include/ovhip.h OVH_BATCH_SLOTS: batches in flight per context
 
 
 class DeviceBackend:

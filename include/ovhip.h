@@ -154,9 +154,12 @@ int ovh_cache_stats(ovh_ctx* ctx, uint64_t stats[3]);
  * voter field: consensus.rs:169-175), the batch is checked as prod_g e(sum_{i in g} r_i pk_i, H_g)
  * e(-G1, sum_i r_i sigma_i) == 1 with one hash_to_G2 and one Miller loop per distinct hash
  * (per vote only the key and signature checks and r_i pk_i), then bisected per vote on failure;
- * the codes are the per-call codes as for any batch. Counters since ovh_create: stats[0] such
- * batches, stats[1] their votes, stats[2] their distinct hashes. The environment variable
- * OVH_SAMEMSG=0 (read at ovh_create) turns the path off. */
+ * the codes are the per-call codes as for any batch. By default the path takes batches of more
+ * than OVH_SMALL_MAX (1,024) votes: below that the small-batch path (one wave per vote, one final
+ * exponentiation) has the lower latency. The environment variable
+ * OVH_SAMEMSG (read at ovh_create) selects 0 = never, 1 = above the small-batch size (default),
+ * 2 = every batch with at most n / 2 distinct hashes (the least device work per vote). Counters
+ * since ovh_create: stats[0] such batches, stats[1] their votes, stats[2] their distinct hashes. */
 int ovh_samemsg_stats(ovh_ctx* ctx, uint64_t stats[3]);
 /* Message cache of the per-call verify (ovh_verify, ovh_verify_batch with n = 1): H =
  * hash_to_G2(hash) of the last 256 hashes verified per call, so every later vote on a hash (all
@@ -211,9 +214,21 @@ int ovh_batch_fallback_device(ovh_ctx* ctx, size_t n, int32_t* d_codes);
  * k + 1's per-vote work. Up to OVH_BATCH_SLOTS batches may be in flight per context; the
  * d_codes of a batch must stay untouched until ovh_batch_wait returns, after which they hold
  * exactly the per-vote ovh_verify results. */
-#define OVH_BATCH_SLOTS 3 /* batches in flight per context (state slots) */
+#define OVH_BATCH_SLOTS 6 /* batches in flight per context (state slots) */
 int ovh_verify_batch_device_async(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
                                   const uint8_t* d_pks, int32_t* d_codes);
+/* The pipelined same-message form: n votes in device memory that all sign the 32-byte `hash`
+ * (host memory, read before the call returns) -- a round's precommits. One hash_to_G2 and one
+ * key-sum Miller loop for the batch, the per-vote key and signature checks and RLC products on
+ * two per-vote streams in turn (consecutive batches co-resident); codes
+ * as ovh_verify_batch_device_async (exactly the per-vote ovh_verify results after
+ * ovh_batch_wait, the same OVH_BATCH_SLOTS limit). The inputs are read after the caller's work
+ * enqueued on ovh_stream before the call, and -- unlike that API's -- must stay untouched until
+ * ovh_batch_wait returns, like the codes. Replaces,
+ * for a round's votes, overlord calling Crypto::verify_signature (consensus.rs:397-416) once per
+ * SignedVote. Single-device contexts. */
+int ovh_verify_samemsg_device_async(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* hash,
+                                    const uint8_t* d_pks, int32_t* d_codes);
 /* The pipelined form with host buffers, for single- and multi-device contexts (a node with no
  * torch; ovh_create_multi is its multi-GPU path): the inputs are copied into pinned staging
  * before the call returns (the caller may reuse them at once); `codes` (host, n entries) must

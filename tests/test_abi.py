@@ -56,3 +56,10 @@ def test_no_cpu_fallback_when_library_missing(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "_lib", None)
     with pytest.raises(RuntimeError):
         _lib.load()
+
+
+def test_batch_slots_mirrored_in_shard():
+    """shard.py's partial rows (one per batch in flight) follow include/ovhip.h OVH_BATCH_SLOTS."""
+    from consensus_overlord_amd.shard import BATCH_SLOTS
+    src = open(os.path.join(ROOT, "include", "ovhip.h")).read()
+    assert int(re.search(r"#define OVH_BATCH_SLOTS (\d+)", src).group(1)) == BATCH_SLOTS

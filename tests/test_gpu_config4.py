@@ -122,11 +122,11 @@ def golden_negs():
             and c["code"] != 0]
 
 
-@pytest.mark.parametrize("devices,nb,n", [([0, 0], 4, 8192), (None, 5, 1024)])
+@pytest.mark.parametrize("devices,nb,n", [([0, 0], 4, 8192), (None, 8, 1024)])
 def test_pipelined_host_batches(golden_negs, devices, nb, n):
     """ovh_verify_batch_async: four 8,192-vote batches over a two-device context ({0, 0}: two
-    device pipelines, rotating final device) and five 1,024-vote batches on one context (the ring
-    of three slots wraps), invalid votes in flight in every batch and half the voters in the
+    device pipelines, rotating final device) and eight 1,024-vote batches on one context (the ring
+    of OVH_BATCH_SLOTS = 6 slots wraps), invalid votes in flight in every batch and half the voters in the
     validator table (table / other split per shard); every batch's codes equal the oracle's."""
     import consensus_overlord_amd as coa
     from consensus_overlord_amd.crypto import Context

@@ -37,6 +37,17 @@ def _round(ctx, lo, n, digest):
     return sigs, pks
 
 
+def _cc(key_hex, mode="2"):
+    """A context whose batches take the same-message path at any size (OVH_SAMEMSG=2; by default
+    only batches above the small-batch size do, include/ovhip.h)."""
+    import consensus_overlord_amd as coa
+    os.environ["OVH_SAMEMSG"] = mode
+    try:
+        return coa.ConsensusCrypto(bytes.fromhex(key_hex * 32))
+    finally:
+        del os.environ["OVH_SAMEMSG"]
+
+
 def _named(golden, name, field):
     return np.frombuffer(bytes.fromhex([c for c in golden["verify"] if c["name"] == name][0][field]), dtype=np.uint8)
 
@@ -47,7 +58,7 @@ def test_relayer_round_99_of_100_prefetch_then_hits(golden):
     the same-message path, and every later verify_signature is a cache hit equal to orc.verify."""
     import consensus_overlord_amd as coa
     from consensus_overlord_amd.crypto import ConsensusError, CryptoErr
-    cc = coa.ConsensusCrypto(bytes.fromhex("6b" * 32))
+    cc = _cc("6b")
     digest = sv.sha(b"samemsg round 7")
     sigs, pks = _round(cc.ctx, 81000, 100, digest)
     cc.update_pubkeys([bytes(p) for p in pks])
@@ -81,7 +92,7 @@ def test_mixed_table_and_keys_three_hashes():
     """A backlog of prevotes, precommits and chokes (three hashes) whose voters are partly in the
     validator table: codes equal the oracle's, one same-message batch, both key sources."""
     import consensus_overlord_amd as coa
-    cc = coa.ConsensusCrypto(bytes.fromhex("6c" * 32))
+    cc = _cc("6c")
     ds = [sv.sha(b"prevote 9"), sv.sha(b"precommit 9"), sv.sha(b"choke 9")]
     S, H, K = [], [], []
     for d, n in zip(ds, (60, 60, 10)):
@@ -109,7 +120,7 @@ def test_hash_whose_every_vote_fails_and_all_valid_batches():
     """A hash whose every vote fails contributes e(O, H) = 1 (its key sum is the identity): the
     other hash's votes still pass without bisection; an all-valid round passes as a whole."""
     import consensus_overlord_amd as coa
-    cc = coa.ConsensusCrypto(bytes.fromhex("6d" * 32))
+    cc = _cc("6d")
     da, db = sv.sha(b"round a"), sv.sha(b"round b")
     sa, pa = _round(cc.ctx, 83000, 40, da)
     sb, pb = _round(cc.ctx, 83100, 24, db)
@@ -136,8 +147,10 @@ def test_hash_whose_every_vote_fails_and_all_valid_batches():
 
 
 def test_samemsg_4096_one_hash_with_invalid_votes():
-    """Config-3 keys all signing one hash (4,096 votes, one same-message batch): 1% sigma + G2 at
-    seeded positions, every position flagged and the rest Ok, as the oracle on a sample."""
+    """Config-3 keys all signing one hash (4,096 votes: the default routing takes the same-message
+    path above the small-batch size): 1% sigma + G2 at seeded positions, every position flagged
+    and the rest Ok, as the oracle on a sample; a 99-vote round on the default context takes the
+    small-batch path (the lower latency) with the same codes."""
     import consensus_overlord_amd as coa
     cc = coa.ConsensusCrypto(bytes.fromhex("6e" * 32))
     n = 4096
@@ -147,8 +160,43 @@ def test_samemsg_4096_one_hash_with_invalid_votes():
     for i in bad:
         sigs[i] = np.frombuffer(sv.add_g2(bytes(sigs[i])), dtype=np.uint8)
     hs = [d] * n
+    b0 = cc.samemsg_stats()
     got = cc.verify_batch(list(map(bytes, sigs)), hs, list(map(bytes, pks)))
+    assert cc.samemsg_stats()[0] == b0[0] + 1
     assert [i for i in range(n) if got[i] != 0] == bad
     assert set(got[bad].tolist()) == {5}
     for i in bad[:3] + [1, 2000, 4095]:
         assert orc.verify(bytes(sigs[i]), d, bytes(pks[i])) == got[i]
+    small = cc.verify_batch(list(map(bytes, sigs[:99])), hs[:99], list(map(bytes, pks[:99])))
+    assert small.tolist() == got[:99].tolist() and cc.samemsg_stats()[0] == b0[0] + 1
+
+
+def test_device_async_pipeline_codes_equal_oracle():
+    """ovh_verify_samemsg_device_async: five batches in flight over two hashes and two sizes (the
+    one-hash plan is rebuilt when n changes), invalid votes (sigma + G2, another voter's
+    signature, a key that does not parse) in some of them; after batch_wait every code equals the
+    oracle's per-vote verify."""
+    import torch
+    import consensus_overlord_amd as coa
+    from consensus_overlord_amd import device as dev
+    cc = coa.ConsensusCrypto(bytes.fromhex("6f" * 32))
+    da, db = sv.sha(b"pipelined a"), sv.sha(b"pipelined b")
+    sa, pa = _round(cc.ctx, 84000, 300, da)
+    sb, pb = _round(cc.ctx, 84000, 300, db)
+    bad = sa.copy()
+    bad[7] = np.frombuffer(sv.add_g2(bytes(bad[7])), dtype=np.uint8)
+    bad[150] = bad[151]
+    badk = pa.copy()
+    badk[299] = np.frombuffer(bytes.fromhex("ff" * 48), dtype=np.uint8)
+    jobs = [(sa, da, pa), (bad, da, badk), (sb, db, pb), (sb[:129], db, pb[:129]), (bad, da, pa)]
+    codes = [torch.full((len(s),), -1, dtype=torch.int32, device="cuda") for s, _, _ in jobs]
+    # the device inputs stay referenced until batch_wait (the library reads them on its own stream)
+    dins = [(torch.from_numpy(s).cuda(), torch.from_numpy(p).cuda()) for s, _, p in jobs]
+    torch.cuda.synchronize()
+    for (_, d, _), (s_d, p_d), c in zip(jobs, dins, codes):
+        dev.verify_samemsg_async(cc.ctx, s_d, d, p_d, c)
+    dev.batch_wait(cc.ctx)
+    for (s, d, p), c in zip(jobs, codes):
+        want = sv.oracle_codes(s, np.tile(np.frombuffer(d, dtype=np.uint8), (len(s), 1)), p)
+        assert c.cpu().numpy().tolist() == want.tolist()
+    assert codes[1].cpu().numpy()[[7, 150, 299]].tolist() != [0, 0, 0]
