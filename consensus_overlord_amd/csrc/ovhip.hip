@@ -1963,8 +1963,8 @@ struct ovh_ctx {
   // SIMD with a vote wave and takes longer than a vote kernel there).
   hipStream_t fstream = nullptr, fstream2 = nullptr;
   hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse; lazy)
-  hipStream_t hstream[OVH_BATCH_SLOTS] = {};  // a same-message batch's hash_to_G2, per slot (lazy)
-  hipStream_t vstream[2] = {};  // ovh_verify_samemsg_device_async's per-vote streams, in turn (lazy)
+  // ovh_verify_samemsg_device_async: [0], [1] the per-vote streams, in turn; [2] hash_to_G2 (lazy)
+  hipStream_t vstream[3] = {};
   hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
@@ -2948,17 +2948,24 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   const hipStream_t fst = c->fs[slot];
   hipStream_t st = c->stream;
   if (one) {
-    hipStream_t& v = c->vstream[c->pipe_k & 1];
-    if (!v) HIPCHK(hipStreamCreateWithFlags(&v, hipStreamNonBlocking));
-    st = v;
+    for (hipStream_t& v : c->vstream)
+      if (!v) {  // high priority: that pool's hardware queues hold only these three streams
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        HIPCHK(hipStreamCreateWithPriority(&v, hipStreamNonBlocking, hi));
+      }
+    st = c->vstream[c->pipe_k & 1];
   }
-  // hash_to_G2 per hash on the slot's own stream (normal priority, beside the per-vote programs:
-  // at the final streams' low priority it took 2.8 ms beside 1,024 vsame waves, r04g; one stream
-  // per slot, so pipelined batches' hash_to_G2 chains overlap instead of queueing behind each
-  // other and the key sums)
-  if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-  if (!c->hstream[slot]) HIPCHK(hipStreamCreateWithFlags(&c->hstream[slot], hipStreamNonBlocking));
-  const hipStream_t xs = c->xstream, hs = c->hstream[slot];
+  // hash_to_G2 per hash beside the per-vote programs at normal priority (at the final streams'
+  // low priority it took 2.8 ms beside 1,024 vsame waves, r04g): on the side stream for a staged
+  // batch; for the one-hash API on ovh_stream itself, which carries nothing else of the batch.
+  // HIP maps streams onto GPU_MAX_HW_QUEUES (4) hardware queues per priority, and two streams on
+  // one queue run in order: a stream per slot for hash_to_G2 landed on the per-vote streams'
+  // queues and serialised them (r04m trace), and on ovh_stream it delayed the next batch's
+  // per-vote work (r04n), so the one-hash path runs on three high-priority streams (a pool of
+  // their own: the two per-vote streams and this one) and the final streams (its key sums there).
+  if (!one && !c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+  const hipStream_t xs = one ? fst : c->xstream, hs = one ? c->vstream[2] : c->xstream;
   HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));  // the inputs (and the slot free: take_slot)
   HIPCHK(hipStreamWaitEvent(hs, c->ev_front[slot], 0));
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
@@ -2987,8 +2994,10 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   uint32_t m = (G + 3) / 4;
   k_samemsg_fix<<<nblk(n), WG, 0, fst>>>(N, gid, ghinf, dc, P);
   // the per-hash key sums, Miller loops and their fold on the side stream, beside the MSM
-  HIPCHK(hipEventRecord(c->ev_x[2], fst));
-  HIPCHK(hipStreamWaitEvent(xs, c->ev_x[2], 0));
+  if (xs != fst) {
+    HIPCHK(hipEventRecord(c->ev_x[2], fst));
+    HIPCHK(hipStreamWaitEvent(xs, c->ev_x[2], 0));
+  }
   {
     StageScope p(c, ST_FOLD, xs);
     const std::vector<uint32_t>& lo = *pl.level_off;
@@ -3008,8 +3017,10 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   }
   if (G > 1) CHK(fold_down(c, slot, xs, 1, &reg, &m, 1));
   CHK(enqueue_msm(c, fst, slot, N, dc));
-  HIPCHK(hipEventRecord(c->ev_x[3], xs));
-  HIPCHK(hipStreamWaitEvent(fst, c->ev_x[3], 0));
+  if (xs != fst) {
+    HIPCHK(hipEventRecord(c->ev_x[3], xs));
+    HIPCHK(hipStreamWaitEvent(fst, c->ev_x[3], 0));
+  }
   int32_t* verdict = c->result + RES_BATCH + slot;
   {
     StageScope p(c, ST_FINAL, fst);
@@ -3608,9 +3619,7 @@ int ovh_multi_peer_matrix(ovh_ctx* c, uint8_t* out, size_t cap) {
 static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1]})
-    if (s) (void)hipStreamSynchronize(s);
-  for (hipStream_t s : c->hstream)
+  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2]})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
@@ -3639,9 +3648,7 @@ static void destroy_one(ovh_ctx* c) {
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1]})
-    if (s) (void)hipStreamDestroy(s);
-  for (hipStream_t s : c->hstream)
+  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2]})
     if (s) (void)hipStreamDestroy(s);
   delete c;
 }
