@@ -411,10 +411,75 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
 // next phase on (tools/fpvm/sched.py), so the next phase's loads may issue while this phase's
 // stores are still in flight.
 #if defined(__HIPCC__)
+// Side words (programs scheduled with spills, tools/fpvm/sched.py spill_pass): one uint32 per
+// lane per phase, bit 31 valid, bit 30 fill (else spill), bits 0..10 the slot, bits 11..22 the
+// scratch entry (12 words at scr + 12 entry, the unit's own scratch). A spill stores its slot
+// after the phase's op; a fill's load is issued at the start of the phase before its own (the
+// previous iteration reads the next phase's side word) and written to its slot after that
+// phase's op and spills -- so the slot is valid from its phase on, and one phase hides the
+// load. Fills
+// read through `nt` loads (L2-served, never a stale L1 line); a spill's store precedes any fill
+// of its entry by >= 2 phases (spill_pass gap).
+constexpr uint32_t SIDE_VALID = 1u << 31, SIDE_FILL = 1u << 30;
+
+__device__ __forceinline__ void side_spill(uint32_t sw, uint32_t* __restrict__ slots, uint32_t* __restrict__ scr) {
+  if ((sw & (SIDE_VALID | SIDE_FILL)) == SIDE_VALID) {
+    const u32x4* s = reinterpret_cast<const u32x4*>(slots + (sw & 0x7FF) * 12);
+    const u32x4 a = s[0], b = s[1], c = s[2];
+    u32x4* d = reinterpret_cast<u32x4*>(scr + ((sw >> 11) & 0xFFF) * 12);
+    d[0] = a;
+    d[1] = b;
+    d[2] = c;
+  }
+}
+
+template <bool SIDE = false>
 __device__ __forceinline__ void run(const uint4* __restrict__ code, uint32_t nphases, uint32_t W, uint32_t lane,
                                     bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
-                                    uint64_t scalar, const Out& out, uint64_t* __restrict__ trace = nullptr) {
+                                    uint64_t scalar, const Out& out, uint64_t* __restrict__ trace = nullptr,
+                                    const uint32_t* __restrict__ side = nullptr, uint32_t* __restrict__ scr = nullptr) {
   static_assert(PREFETCH == 4, "prefetch ring below is 4 deep");
+  if constexpr (SIDE) {
+    uint4 q0 = code[lane], q1 = code[(size_t)W + lane], q2 = code[(size_t)2 * W + lane],
+          q3 = code[(size_t)3 * W + lane];
+    uint32_t s0 = side[lane], s1 = side[W + lane], s2 = side[2 * W + lane], s3 = side[3 * W + lane];
+    // inactive lanes (a slice past the batch's end) run no side op: their unit has no scratch
+    if (!active) s0 = s1 = s2 = s3 = 0;
+#pragma unroll 1
+    for (uint32_t ph = 0; ph < nphases; ++ph) {
+      const uint4 cur = q0;
+      q0 = q1;
+      q1 = q2;
+      q2 = q3;
+      q3 = code[(size_t)(ph + PREFETCH) * W + lane];
+      const uint32_t sw = s0;
+      s0 = s1;
+      s1 = s2;
+      s2 = s3;
+      s3 = active ? side[(size_t)(ph + PREFETCH) * W + lane] : 0u;
+      // the fill of phase ph + 1 (its side word is s0 now): issue the load before this phase
+      const bool fill = (s0 & (SIDE_VALID | SIDE_FILL)) == (SIDE_VALID | SIDE_FILL);
+      u32x4 f0, f1, f2;
+      if (fill) {
+        const u32x4* src = reinterpret_cast<const u32x4*>(scr + ((s0 >> 11) & 0xFFF) * 12);
+        f0 = __builtin_nontemporal_load(src);
+        f1 = __builtin_nontemporal_load(src + 1);
+        f2 = __builtin_nontemporal_load(src + 2);
+      }
+      exec(cur, active, slots, cst, scalar, out);
+      // this phase's spill reads its slot before the fill lands: a fill may take the slot of a
+      // value whose last read is this spill
+      side_spill(sw, slots, scr);
+      if (fill) {
+        u32x4* d = reinterpret_cast<u32x4*>(slots + (s0 & 0x7FF) * 12);
+        d[0] = f0;
+        d[1] = f1;
+        d[2] = f2;
+      }
+    }
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    return;
+  }
   // trace (diagnostics, OVH_FLAG_VM_TRACE): wall clock after every phase
   if (trace && threadIdx.x == 0) trace[0] = wall_clock64();
   // instructions are prefetched PREFETCH phases ahead (an HBM / L2 round trip outlasts a light

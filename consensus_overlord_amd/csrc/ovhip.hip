@@ -218,7 +218,10 @@ struct VmDev {  // a program in device memory
   const uint16_t* out;
   uint64_t* trace;  // OVH_FLAG_VM_TRACE: nphases + 1 timestamps of workgroup 0, else null
   uint64_t* clk;    // OVH_FLAG_VM_CLOCK (vote / vote_t): per workgroup (d memtime, d realtime), else null
+  const uint32_t* side;  // spilled programs (vote / vote_t): per-lane side words (fpvm.hpp run), else null
 };
+// per-vote scratch of the spilled vote programs (tools/fpvm/gen.py SPILL_K): entries of 12 words
+constexpr uint32_t VOTE_NSCR = VM_VOTE_NSCR > VM_VOTE_T_NSCR ? VM_VOTE_NSCR : VM_VOTE_T_NSCR;
 
 // OVH_FLAG_VM_CLOCK: shader-cycle and 100 MHz stamps around a workgroup's program (diagnostic
 // runs of the measurement only; a null pointer executes no stamp). Capacity: VM_CLOCK_WGS
@@ -336,7 +339,7 @@ __device__ __forceinline__ void vote_stagger() {
 __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
                                                 const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
                                                 Slab s, uint64_t seed, uint64_t base, int32_t* __restrict__ codes,
-                                                Slab part0, unsigned long long* vstart) {
+                                                Slab part0, unsigned long long* vstart, uint32_t* __restrict__ scr) {
   __builtin_amdgcn_s_setprio(2);  // per-vote stages outrank a co-resident final-stream wave
   if (vstart && threadIdx.x == 0) atomicAdd(vstart, 1ull);  // resident (k_gate)
   extern __shared__ uint4 lds4[];
@@ -376,9 +379,9 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
   vote_stagger();
   ClockStamp cs;
   cs.begin(prog.clk);
-  vm::run(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst, vote_scalar(seed, base, i),
-          vm::Out{s.p, s.cap, i},
-          blockIdx.x == 0 ? prog.trace : nullptr);
+  vm::run<(VM_VOTE_NSCR > 0)>(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst,
+                              vote_scalar(seed, base, i), vm::Out{s.p, s.cap, i},
+                              blockIdx.x == 0 ? prog.trace : nullptr, prog.side, scr + (size_t)i * VOTE_NSCR * 12);
   cs.end(prog.clk);
   if (active && lane == 0) {
     const uint32_t pf = hdr[0];
@@ -485,7 +488,7 @@ struct PkSrc {
 __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
                                                   PkSrc pk, const uint8_t* __restrict__ sigs, Slab s, uint64_t seed,
                                                   uint64_t base, int32_t* __restrict__ codes, Slab part0,
-                                                  unsigned long long* vstart) {
+                                                  unsigned long long* vstart, uint32_t* __restrict__ scr) {
   __builtin_amdgcn_s_setprio(2);
   if (vstart && threadIdx.x == 0) atomicAdd(vstart, 1ull);
   extern __shared__ uint4 lds4[];
@@ -521,8 +524,9 @@ __global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev 
   vote_stagger();
   ClockStamp cs;
   cs.begin(prog.clk);
-  vm::run(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst, vote_scalar(seed, base, i),
-          vm::Out{s.p, s.cap, i}, blockIdx.x == 0 ? prog.trace : nullptr);
+  vm::run<(VM_VOTE_T_NSCR > 0)>(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst,
+                                vote_scalar(seed, base, i), vm::Out{s.p, s.cap, i},
+                                blockIdx.x == 0 ? prog.trace : nullptr, prog.side, scr + (size_t)i * VOTE_NSCR * 12);
   cs.end(prog.clk);
   if (active && lane == 0) {
     const uint32_t sf = hdr[0], pf = hdr[1];
@@ -1969,6 +1973,7 @@ struct ovh_ctx {
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
   uint32_t* state_slot[OVH_BATCH_SLOTS] = {};
+  uint32_t* vscr[OVH_BATCH_SLOTS] = {};  // the spilled vote programs' per-vote scratch (VOTE_NSCR entries)
   uint32_t* red_slot[OVH_BATCH_SLOTS] = {};  // fold regions R0..R3 (R1: the 16-vote groups)
   int32_t* grp_ok[OVH_BATCH_SLOTS] = {};
   uint32_t slot_n[OVH_BATCH_SLOTS] = {};
@@ -2037,6 +2042,10 @@ struct ovh_ctx {
   // 0: off; 1 (default): batches above small_max votes (below it the small-batch path has the
   // lower latency); 2: every batch with at most n / 2 distinct hashes
   int samemsg = 1;
+  // pipelined batches (ovh_verify_batch_device_async): consecutive batches' hash_to_field + vote
+  // kernels on the two per-vote streams in turn, so two batches' vote grids co-reside (the
+  // spilled vote program's LDS fits seven workgroups per CU); OVH_VOTE_PAIR=0: all on `stream`
+  bool vote_pair = VOTE_NSCR > 0;
   uint64_t sm_batches = 0, sm_votes = 0, sm_hashes = 0;
   // ovh_verify_samemsg_device_async: the one-hash plan of sm1_n votes (gid = 0 | head 0 | pairs)
   // and its level offsets; the hash of each slot (32 B per slot)
@@ -2137,7 +2146,8 @@ static_assert(FOLD_STRIDE_W <= VM_SLICES * VOTE_STRIDE_W && FOLD_STRIDE_W <= VM_
               "fused fold reuses the vote slots");
 
 static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphases, uint32_t W, uint32_t NW,
-                     const uint16_t* in, uint32_t nin, const uint16_t* out, uint32_t nout) {
+                     const uint16_t* in, uint32_t nin, const uint16_t* out, uint32_t nout,
+                     const uint32_t* side = nullptr) {
   // + PREFETCH trailing NOP phases (instruction prefetch)
   const size_t words = (size_t)nphases * W * NW, pad = (size_t)vm::PREFETCH * W * NW;
   void *dc = nullptr, *di = nullptr, *dout = nullptr;
@@ -2157,6 +2167,15 @@ static int vm_upload(ovh_ctx* c, VmDev& d, const uint32_t* code, uint32_t nphase
   d.out = (const uint16_t*)dout;
   d.trace = nullptr;
   d.clk = nullptr;
+  d.side = nullptr;
+  if (side) {  // nphases x W side words + PREFETCH phases of zeros
+    void* ds = nullptr;
+    HIPCHK(hipMalloc(&ds, ((size_t)nphases + vm::PREFETCH) * W * 4));
+    c->vm_bufs.push_back(ds);
+    HIPCHK(hipMemcpy(ds, side, (size_t)nphases * W * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset((uint32_t*)ds + (size_t)nphases * W, 0, (size_t)vm::PREFETCH * W * 4));
+    d.side = (const uint32_t*)ds;
+  }
   if ((c->flags & OVH_FLAG_VM_CLOCK) && (code == VM_VOTE_CODE || code == VM_VOTE_T_CODE)) {
     void* dk = nullptr;
     HIPCHK(hipMalloc(&dk, (size_t)2 * VM_CLOCK_WGS * 8));
@@ -2178,9 +2197,21 @@ static int vm_init(ovh_ctx* c) {
   HIPCHK(hipMalloc(&c->vm_consts, sizeof(VM_CONST_WORDS)));
   HIPCHK(hipMemcpy(c->vm_consts, VM_CONST_WORDS, sizeof(VM_CONST_WORDS), hipMemcpyHostToDevice));
   CHK(vm_upload(c, c->vm_vote, VM_VOTE_CODE, VM_VOTE_NPHASES, VM_VOTE_W, VM_VOTE_NW, VM_VOTE_IN, VM_VOTE_NIN, VM_VOTE_OUT,
-                VM_VOTE_NOUT));
+                VM_VOTE_NOUT,
+#if VM_VOTE_NSCR > 0
+                VM_VOTE_SIDE
+#else
+                nullptr
+#endif
+                ));
   CHK(vm_upload(c, c->vm_vote_t, VM_VOTE_T_CODE, VM_VOTE_T_NPHASES, VM_VOTE_T_W, VM_VOTE_T_NW, VM_VOTE_T_IN, VM_VOTE_T_NIN,
-                VM_VOTE_T_OUT, VM_VOTE_T_NOUT));
+                VM_VOTE_T_OUT, VM_VOTE_T_NOUT,
+#if VM_VOTE_T_NSCR > 0
+                VM_VOTE_T_SIDE
+#else
+                nullptr
+#endif
+                ));
   CHK(vm_upload(c, c->vm_fold, VM_FOLD_CODE, VM_FOLD_NPHASES, VM_FOLD_W, VM_FOLD_NW, VM_FOLD_IN, VM_FOLD_NIN, VM_FOLD_OUT,
                 VM_FOLD_NOUT));
   CHK(vm_upload(c, c->vm_final, VM_FINAL_CODE, VM_FINAL_NPHASES, VM_FINAL_W, VM_FINAL_NW, VM_FINAL_IN, VM_FINAL_NIN, VM_FINAL_OUT,
@@ -2331,9 +2362,10 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
   while (cap < n) cap <<= 1;
   CHK(sync_all(c));
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
-    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k]})
+    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
+                    (void*)c->vscr[k]})
       if (p) (void)hipFree(p);
-    c->state_slot[k] = c->red_slot[k] = c->msm_buf[k] = nullptr;
+    c->state_slot[k] = c->red_slot[k] = c->msm_buf[k] = c->vscr[k] = nullptr;
     c->grp_ok[k] = nullptr;
     c->slot_n[k] = 0;
   }
@@ -2345,6 +2377,7 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
     HIPCHK(hipMalloc(&c->red_slot[k], (size_t)4 * PART_PLANES * 12 * c->red_cap * 4));
     HIPCHK(hipMalloc(&c->grp_ok[k], ((size_t)cap / GROUP_VOTES + 1) * 4));
     HIPCHK(hipMalloc(&c->msm_buf[k], msm_words(cap) * 4));
+    if (VOTE_NSCR) HIPCHK(hipMalloc(&c->vscr[k], (size_t)cap * VOTE_NSCR * 12 * 4));
   }
   c->cap = cap;
   return 0;
@@ -2427,9 +2460,9 @@ struct KeySrc {
 // (-> R0), fold level 1 (-> R1: one partial per 16-vote group). alone: the batch's combined
 // check covers only this batch (not a shard of a larger combined check).
 static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
-                       int32_t* d_codes, bool fold1 = true, bool alone = false) {
+                       int32_t* d_codes, bool fold1 = true, bool alone = false, hipStream_t vst = nullptr) {
   Slab s{c->state_slot[slot], c->cap};
-  hipStream_t st = c->stream;
+  hipStream_t st = vst ? vst : c->stream;
   c->ev_mask = 0;
   uint64_t seed, base;
   CHK(draw_seed(c, &seed, &base));
@@ -2442,23 +2475,23 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
   {  // hash_to_field on the main stream: its inputs are ready in that stream's order (the
      // staging copies, or a caller's writes on ovh_stream)
-    StageScope p(c, ST_H2F);
+    StageScope p(c, ST_H2F, st);
     k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s);
   }
   {
-    StageScope p(c, ST_VOTE);
+    StageScope p(c, ST_VOTE, st);
     if (key.bytes)
       k_vm_vote<<<nwg, 64, LDS_VOTE, st>>>(n, c->vm_vote, c->vm_fold, c->vm_consts, key.bytes, d_sigs, s, seed, base,
-                                           d_codes, region_F(c, slot, 0), c->vstart);
+                                           d_codes, region_F(c, slot, 0), c->vstart, c->vscr[slot]);
     else
       k_vm_vote_t<<<nwg, 64, LDS_VOTE_T, st>>>(n, c->vm_vote_t, c->vm_fold, c->vm_consts, key.pts, d_sigs, s, seed,
-                                               base, d_codes, region_F(c, slot, 0), c->vstart);
+                                               base, d_codes, region_F(c, slot, 0), c->vstart, c->vscr[slot]);
     c->vlaunched += nwg;
     c->clk_wgs = nwg < VM_CLOCK_WGS ? nwg : VM_CLOCK_WGS;
     c->clk_table = key.bytes == nullptr;
   }
   if (fold1) {  // fold level 1: R0 -> R1 (one partial per 16-vote group)
-    StageScope p(c, ST_FOLD);
+    StageScope p(c, ST_FOLD, st);
     const uint32_t m1 = (nwg + 3) / 4;
     k_vm_fold<VM_FOLD_UNITS><<<(m1 + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(
         nwg, c->vm_fold, c->vm_consts, region_F(c, slot, 0), region_S(c, slot, 0), region_F(c, slot, 1), nullptr);
@@ -2588,9 +2621,10 @@ static void enqueue_bisect(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, int
 // The final stream of `slot` after the vote kernel (batch_front without fold level 1): waits for
 // it, with `pipe` also for the next batch's vote workgroups to be resident (k_gate), then the
 // fold levels R0 -> R1 -> ... down to <= until partials (*reg, *m).
-static int side_front(ovh_ctx* c, int slot, uint32_t n, bool pipe, uint32_t until, int* reg, uint32_t* m) {
+static int side_front(ovh_ctx* c, int slot, uint32_t n, bool pipe, uint32_t until, int* reg, uint32_t* m,
+                      hipStream_t vst = nullptr) {
   hipStream_t fst = c->fs[slot];
-  HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
+  HIPCHK(hipEventRecord(c->ev_front[slot], vst ? vst : c->stream));
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
   if (pipe) k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
@@ -2740,17 +2774,31 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
   int slot;
   CHK(take_slot(c, &slot));
   const bool side = c->fold_side;
-  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, !side, true));
+  // pipelined: this batch's per-vote kernels on one of the two per-vote streams (vote_pair),
+  // after the caller's work on `stream` and the slot's release (take_slot)
+  hipStream_t vst = c->stream;
+  if (pipe && c->vote_pair) {
+    for (int k = 0; k < 2; ++k)
+      if (!c->vstream[k]) {
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        HIPCHK(hipStreamCreateWithPriority(&c->vstream[k], hipStreamNonBlocking, hi));
+      }
+    vst = c->vstream[slot & 1];
+    HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
+    HIPCHK(hipStreamWaitEvent(vst, c->ev_front[slot], 0));
+  }
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, !side, true, vst));
   hipStream_t fst = c->fs[slot];
   uint32_t m = groups_of((uint32_t)n);
   int reg = 1;
   if (side) {  // fold levels on the final stream, beside the next batch's vote kernel
-    CHK(side_front(c, slot, (uint32_t)n, pipe, 4, &reg, &m));
+    CHK(side_front(c, slot, (uint32_t)n, pipe, 4, &reg, &m, vst));
   } else {
     // every fold level on the main stream (it idles while a final runs): the final streams carry
     // only the MSM, the finals and the bisections
-    CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 4));
-    HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
+    CHK(fold_down(c, slot, vst, VM_SLICES, &reg, &m, 4));
+    HIPCHK(hipEventRecord(c->ev_front[slot], vst));
     HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
     if (pipe) {
       const uint32_t nwg = ((uint32_t)n + VM_SLICES - 1) / VM_SLICES;
@@ -3516,6 +3564,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   if (const char* e = getenv("OVH_FOLD_SIDE")) c->fold_side = atoi(e) != 0;
   if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
   if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e);
+  if (const char* e = getenv("OVH_VOTE_PAIR")) c->vote_pair = atoi(e) != 0;
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->wg_cap = 4u * (uint32_t)ncu;
@@ -3623,7 +3672,7 @@ static void destroy_one(ovh_ctx* c) {
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
-                    (void*)c->gslab[k]})
+                    (void*)c->gslab[k], (void*)c->vscr[k]})
       if (p) (void)hipFree(p);
   for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vstart, (void*)c->vm_consts,
                   (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
@@ -3697,7 +3746,7 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
     else
       k_vm_vote<<<(N + VM_SLICES - 1) / VM_SLICES, 64, LDS_VOTE, st>>>(N, c->vm_vote, c->vm_fold, c->vm_consts,
                                                                       c->in_buf + n * 96, c->in_buf, s, 1, 0, dc,
-                                                                      region_F(c, 0, 0), nullptr);
+                                                                      region_F(c, 0, 0), nullptr, c->vscr[0]);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e1, c->xstream));

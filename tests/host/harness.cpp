@@ -104,13 +104,27 @@ void hx_fp_inv_raw(const uint32_t* a, const uint32_t* r_raw, uint32_t* out) {
 // phase (a phase's writes never target a slot that phase reads: tools/fpvm/sched.py).
 // slots: nslots x 12 words (in/out); planes: `st` output planes, 12 words each.
 // any_all = 1 runs every wave-uniform block for every lane (all phase-header bits set).
+// side / scr (spilled programs, fpvm.hpp run<true>): per-lane side words and the unit's
+// scratch; after a phase's ops, its spills store their slots, then the next phase's fills land.
 int hx_vm_run(const uint32_t* code, uint32_t nphases, uint32_t W, uint32_t NW, const uint32_t* cst, uint32_t* slots,
-              uint64_t scalar, uint32_t* planes, uint32_t nplanes, int any_all) {
+              uint64_t scalar, uint32_t* planes, uint32_t nplanes, int any_all, const uint32_t* side, uint32_t* scr) {
   using namespace ovh::vm;
   const uint32_t all = any_all ? (H_MUL | H_MULNEG | H_FLAG | H_LIN | H_LINNEG | H_ACC | H_RARE | H_SELB) : 0u;
   const ovh::vm::Out out{planes, 1, 0};
   (void)nplanes;
-  for (uint32_t ph = 0; ph < nphases; ++ph)
+  for (uint32_t ph = 0; ph < nphases; ++ph) {
+    if (ph > 0 && side)
+      for (uint32_t lane = 0; lane < W; ++lane) {
+        const uint32_t sw = side[(size_t)(ph - 1) * W + lane];
+        if ((sw >> 30) == 2)  // spill of phase ph - 1
+          for (int k = 0; k < 12; ++k) scr[((sw >> 11) & 0xFFF) * 12 + k] = slots[(sw & 0x7FF) * 12 + k];
+      }
+    if (ph > 0 && side)
+      for (uint32_t lane = 0; lane < W; ++lane) {
+        const uint32_t sw = side[(size_t)ph * W + lane];
+        if ((sw >> 30) == 3)  // fill of phase ph
+          for (int k = 0; k < 12; ++k) slots[(sw & 0x7FF) * 12 + k] = scr[((sw >> 11) & 0xFFF) * 12 + k];
+      }
     for (uint32_t lane = 0; lane < W; ++lane) {
       const uint32_t* w = code + ((size_t)ph * W + lane) * NW;
       ovh::vm::exec(uint4{w[0] | all, w[1], w[2], w[3]}, true, slots, cst, scalar, out);
@@ -122,6 +136,7 @@ int hx_vm_run(const uint32_t* code, uint32_t nphases, uint32_t W, uint32_t NW, c
         if (!br) return -1 - (int)ph;
       }
     }
+  }
   return 0;
 }
 

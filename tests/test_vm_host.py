@@ -51,9 +51,14 @@ def run_vm(hx, consts, sc, words, inputs, scalar, any_all):
     planes = np.zeros(64 * 12, dtype=np.uint32)
     u32p = ctypes.POINTER(ctypes.c_uint32)
     hx.hx_vm_run.argtypes = [u32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, u32p, u32p, ctypes.c_uint64,
-                             u32p, ctypes.c_uint32, ctypes.c_int]
+                             u32p, ctypes.c_uint32, ctypes.c_int, u32p, u32p]
+    # spilled programs (sched.spill_pass): side words and the unit's scratch
+    nscr = getattr(sc, "nscr", 0)
+    side = np.asarray(sc.side_words, dtype=np.uint32) if nscr else None
+    scr = np.zeros(max(nscr, 1) * 12, dtype=np.uint32)
     assert hx.hx_vm_run(code.ctypes.data_as(u32p), sc.nrounds, sc.W, sched.words_per_lane(prog), cst.ctypes.data_as(u32p),
-                        slots.ctypes.data_as(u32p), scalar, planes.ctypes.data_as(u32p), 64, any_all) == 0
+                        slots.ctypes.data_as(u32p), scalar, planes.ctypes.data_as(u32p), 64, any_all,
+                        side.ctypes.data_as(u32p) if side is not None else None, scr.ctypes.data_as(u32p)) == 0
     out = {}
     for name, v in prog.outputs.items():
         op = prog.ops[v]

@@ -64,6 +64,12 @@ SEC_BIAS = {"vote_t": {"sig": 1500}}
 NOMIX = set(filter(None, os.environ.get(
     "OVH_GEN_NOMIX", "vote,vote_t,vote1,vote_t1,vote1h,vote_t1h,final1,qcpre,qcmil,votew,votew_t,signg0,signg1,"
     "sigchk,pkchk,pkgen,vsame,vsame_t,h2g,gmil,pkdec,g1grp").split(",")))
+# r04: the batch vote programs keep at most SPILL_K values in LDS per phase; the rest wait in the
+# vote's global scratch (sched.spill_pass: side-word spills / fills beside the lane ops), so a
+# CU holds seven vote workgroups -- two pipelined batches' grids co-resident -- beside a final
+# (ovhip.hip LDS budget). OVH_GEN_SPILL="vote=0,vote_t=0" builds them without spills.
+SPILL_K = {"vote": 90, "vote_t": 90}
+SPILL_K.update({k: int(v) for k, v in (x.split("=") for x in filter(None, os.environ.get("OVH_GEN_SPILL", "").split(",")))})
 # slots: four vote workgroups (4 x 4 slices) and two finals must share a CU's 160 KiB of LDS
 # (ovhip.hip static_assert); vote 159, final 226 slots with these settings
 
@@ -84,7 +90,7 @@ def build_all():
                 if name in SEC_BIAS and op.sec in SEC_BIAS[name]}
         sc = sched.schedule(prog, WIDTH[name], consts, max_slots=MAX_SLOTS.get(name, 256), heavy_w=HEAVY_W.get(name, 2),
                             hoist=HOIST.get(name), stretch=STRETCH.get(name, 1.3), mixed=name not in NOMIX,
-                            bias=bias or None)
+                            bias=bias or None, spill_k=SPILL_K.get(name) or None)
         words = sched.encode(sc)
         out[name] = (prog, sc, words, ins, outs)
     return consts, out
@@ -112,6 +118,7 @@ def emit(consts, built, path):
         lines.append("#define VM_%s_NW %d" % (N, sched.words_per_lane(prog)))
         lines.append("#define VM_%s_NPHASES %d" % (N, sc.nrounds))
         lines.append("#define VM_%s_NSLOTS %d" % (N, sc.nslots))
+        lines.append("#define VM_%s_NSCR %d" % (N, getattr(sc, "nscr", 0)))
         lines.append("#define VM_%s_NIN %d" % (N, len(ins)))
         lines.append("#define VM_%s_NOUT %d" % (N, len(outs)))
         slot_in = [sc.slot_of.get(prog.inputs[n], 0xFFFF) for n in ins]
@@ -129,6 +136,12 @@ def emit(consts, built, path):
         for k in range(0, len(words), 16):
             lines.append("  " + ",".join("0x%x" % w for w in words[k:k + 16]) + ",")
         lines.append("};")
+        if getattr(sc, "nscr", 0):   # side words (spills / fills), nphases x W
+            sw = sc.side_words
+            lines.append("static const uint32_t VM_%s_SIDE[%d] = {" % (N, len(sw)))
+            for k in range(0, len(sw), 16):
+                lines.append("  " + ",".join("0x%x" % w for w in sw[k:k + 16]) + ",")
+            lines.append("};")
     text = "\n".join(lines) + "\n"
     tmp = path + ".tmp"
     with open(tmp, "w") as fh:

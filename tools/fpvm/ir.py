@@ -395,8 +395,18 @@ class Prog:
     def evaluate(self, inputs: dict, scalar: int = 0) -> list:
         """Evaluate every value with Python integers (canonical values, not Montgomery)."""
         vals = [None] * len(self.ops)
+        # fill ops (sched.spill_pass) are appended after their readers: each takes its original
+        # value's (deps[0]) as soon as that is known
+        fills = {}
         for i, op in enumerate(self.ops):
+            if op.kind == "fill":
+                fills.setdefault(op.deps[0], []).append(i)
+        for i, op in enumerate(self.ops):
+            if op.kind == "fill":
+                continue
             vals[i] = eval_op(op, vals, inputs, scalar)
+            for f in fills.get(i, ()):
+                vals[f] = vals[i]
         return vals
 
 
@@ -421,6 +431,8 @@ def eval_op(op, vals, inputs, scalar):
         return 1 if x == y else 0
     if k == "sop":
         return (g(0) * g(2) + op.coefs[1] * g(1) * g(3)) % P
+    if k == "spill":
+        return g(0)
     if k == "sgn0":
         return vals[s[0]] & 1
     if k == "lex":

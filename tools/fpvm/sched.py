@@ -19,6 +19,7 @@ Instruction (4 x uint32 per lane per phase):
 """
 from __future__ import annotations
 
+import bisect
 import heapq
 import os
 from collections import defaultdict
@@ -26,7 +27,7 @@ from collections import defaultdict
 from ir import CMAX, HALF_P, HEAVY, P, lin_form
 
 OPC = {"nop": 0, "muls": 1, "sgn0": 2, "lex": 3, "inv": 4, "lin": 5, "sel": 6, "eq": 7, "and": 8, "or": 9,
-       "xor": 10, "st": 11, "selb": 12, "sop": 13}
+       "xor": 10, "st": 11, "selb": 12, "sop": 13, "spill": 14, "fill": 15}
 CONST_BASE = 0x800
 ABSENT = 0xFFFF
 # LDS pass width (lanes) and slot residues that share banks (OVH_BANK="lanes,mod" for A/B builds)
@@ -86,15 +87,17 @@ class Scheduled:
     def stats(self):
         heavy_rounds = sum(1 for k in self.kinds if k == "H")
         nheavy = sum(1 for r in self.rounds for i in r if self.prog.ops[i].kind in HEAVY)
-        nlight = sum(1 for r in self.rounds for i in r if self.prog.ops[i].kind not in HEAVY)
+        nlight = sum(1 for r in self.rounds for i in r if self.prog.ops[i].kind not in HEAVY and
+                     self.prog.ops[i].kind not in SIDE)
         return {"phases": self.nrounds, "heavy_phases": heavy_rounds, "light_phases": self.nrounds - heavy_rounds,
                 "heavy_ops": nheavy, "light_ops": nlight, "slots": self.nslots, "W": self.W,
                 "lane_util_heavy": round(nheavy / max(1, heavy_rounds * self.W), 3),
-                "cost_est": heavy_rounds * 900 + (self.nrounds - heavy_rounds) * 150}
+                "cost_est": heavy_rounds * 900 + (self.nrounds - heavy_rounds) * 150,
+                **({"scratch": self.nscr, "spills": self.nspill, "fills": self.nfill} if getattr(self, "nscr", 0) else {})}
 
 
 def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1, mixed=True, slot_target=None,
-             hoist=None, stretch=1.3, split_sop=False, dual=False, bias=None, light_margin=0):
+             hoist=None, stretch=1.3, split_sop=False, dual=False, bias=None, light_margin=0, spill_k=None):
     ops = prog.ops
     live = prog.live_ops()
     liveset = set(live)
@@ -210,6 +213,9 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
                 indeg[s_] -= 1
                 if indeg[s_] == 0:
                     (ready_h if ops[s_].kind in HEAVY else ready_l).append(s_)
+    nscr = nspill = nfill = 0
+    if spill_k is not None:   # at most spill_k values in LDS per phase (spill_pass)
+        nscr, nspill, nfill = spill_pass(prog, rounds, W, spill_k)
     # ---- slot allocation
     def_round = {i: -1 for i in pre if ops[i].kind == "in"}
     for t, r in enumerate(rounds):
@@ -245,7 +251,7 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
     use = defaultdict(lambda: [0] * BANK_MOD)
     seen_c = set()
     for t, r in enumerate(rounds):
-        for k, i in enumerate(r):
+        for k, i in enumerate(x for x in r if ops[x].kind not in SIDE):
             lane_of[i] = k
             g = k // BANK_LANES
             A, B, C, D = lane_operands(prog, i)[:4]
@@ -285,7 +291,7 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
     for t, r in enumerate(rounds):
         free.extend(frees_at.pop(t, []))
         for i in r:
-            if ops[i].kind != "st":
+            if ops[i].kind not in ("st", "spill"):
                 alloc(i)
     if max_slots is not None and nslots > max_slots:
         raise RuntimeError("%s: %d slots > %d" % (prog.name, nslots, max_slots))
@@ -296,6 +302,7 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
             consts.ref(ops[i].imm, ops[i].name == "raw")
     sc = Scheduled(prog, W, rounds, slot_of, nslots, consts)
     sc.kinds = kinds
+    sc.nscr, sc.nspill, sc.nfill = nscr, nspill, nfill
     return sc
 
 
@@ -313,6 +320,8 @@ def improve_banks(prog, rounds, slot_of, def_round, last_use, nslots, consts, pa
     reads_of = defaultdict(set)    # value -> contexts it is read in
     for t, r in enumerate(rounds):
         for i in r:
+            if ops[i].kind in SIDE:
+                continue
             A, B, C, D = lane_operands(prog, i)[:4]
             refs = [(1, B), (2, C)] if ops[i].kind == "selb" else list(enumerate((A, B, C, D)))
             for pos, v in refs:
@@ -460,9 +469,11 @@ def lane_operands(prog, i, unit=False):
     elif k in ("sgn0", "lex"):
         A, B, C, D = s[0], None, None, None
         coefs[:4] = [1, 0, 1, 0]
-    elif k in ("inv", "st"):
+    elif k in ("inv", "st", "spill"):
         A, B, C, D = s[0], None, None, None
         coefs[:4] = [1, 0, 0, 0]
+    elif k == "fill":
+        A, B, C, D = None, None, None, None
     elif k == "sel":           # A = flag, B = x, C = y
         A, B, C, D = s[0], s[1], s[2], None
     elif k == "selb":          # B = x, C = y
@@ -480,7 +491,19 @@ def encode(sc):
     ops = sc.prog.ops
     nw = words_per_lane(sc.prog)
     LW = sc.prog.lin_width
+    sc.side_words = []
     for r in sc.rounds:
+        sides = [i for i in r if ops[i].kind in SIDE]
+        r = [i for i in r if ops[i].kind not in SIDE]
+        assert len(r) <= sc.W and len(sides) <= sc.W
+        # side word per lane: bit 31 valid, bit 30 fill (else spill), bits 0..10 the slot,
+        # bits 11..22 the scratch entry (fpvm.hpp run)
+        sw = [0] * sc.W
+        for k, i in enumerate(sides):
+            v = i if ops[i].kind == "fill" else ops[i].srcs[0]
+            sw[k] = 1 << 31 | (ops[i].kind == "fill") << 30 | sc.slot_of[v] | ops[i].imm << 11
+            assert sc.slot_of[v] < 2048 and ops[i].imm < 4096
+        sc.side_words += sw
         lanes = list(r) + [None] * (sc.W - len(r))
         first = len(words)
         # unit block for this phase's lin ops only when every one of them is a unit sum
@@ -558,7 +581,13 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
     W = sc.W
     nw = words_per_lane(sc.prog)
     stored = {}
+    scratch = {}
+    side = getattr(sc, "side_words", None) or [0] * (sc.nrounds * W)
     for t in range(sc.nrounds):
+        # side ops (fpvm.hpp run): fills land at the start of the phase
+        for sw in side[t * W:(t + 1) * W]:
+            if sw >> 31 and (sw >> 30) & 1:
+                slots[sw & 0x7FF] = scratch[(sw >> 11) & 0xFFF]
         results = []
         for lane in range(W):
             ins = words[(t * W + lane) * nw:(t * W + lane) * nw + nw]
@@ -609,8 +638,181 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
             results.append((dst, z))
         for dst, z in results:
             slots[dst] = z
+        for sw in side[t * W:(t + 1) * W]:   # spills after the phase's ops
+            if sw >> 31 and not (sw >> 30) & 1:
+                scratch[(sw >> 11) & 0xFFF] = slots[sw & 0x7FF]
     out = {}
     for name, v in sc.prog.outputs.items():
         op = sc.prog.ops[v]
         out[name] = stored[op.imm] if op.kind == "st" else slots[sc.slot_of[v]]
     return out
+
+
+SIDE = ("spill", "fill")   # side ops: run beside a phase's lane ops (one per lane per phase)
+
+
+def spill_pass(prog, rounds, W, K, gap=3):
+    """Split long idle stretches of values out of LDS so that at most K values occupy a slot in
+    any phase (r04: two vote workgroups per SIMD need the vote program under ~90 of its 159
+    slots; VERDICT r03 "next" 1).
+
+    Occupancy of a value: [def phase, last read phase] (a slot last read in phase t is free from
+    t + 1: the allocator's rule). Spills and fills are side ops: each lane runs at most one
+    beside its phase op (fpvm.hpp run: a per-lane side word per phase), so they take no lane:
+      spill in phase t  stores a slot to the unit's scratch after the phase's ops (a value
+                        defined in phase t may be stored in t);
+      fill in phase t   writes a slot at the start of phase t from a scratch load issued at the
+                        start of phase t - 1 (one phase hides the L2 latency): it occupies from t.
+    Greedy, Belady-like: at the most crowded phase t*, among the values that occupy t* without
+    being read or defined there, take the one whose next read c is farthest; spill it in the
+    earliest phase from its last read / definition before t* with a side word free (none if an
+    earlier spill left a copy: values are immutable) and fill it in the latest phase <= c with a
+    side word free (its later reads are rewritten to the fill), at least `gap` phases after the
+    spill (the store drains before the load). Each spilled value gets a scratch entry, reused once
+    its last fill has completed (interval colouring). The floor is what one phase reads and
+    defines (at most 80 values at 16 lanes).
+    Mutates prog.ops (appended ops, rewritten srcs), prog.outputs and `rounds` (side ops are
+    appended to their phase's list; encode() emits them as side words); returns (scratch
+    entries, spills, fills)."""
+    from ir import Op
+    ops = prog.ops
+    T = len(rounds)
+    side = [0] * T
+    d = {}
+    uses = defaultdict(list)
+    for name, v in prog.inputs.items():
+        d[v] = -1
+    readers = defaultdict(list)
+    for t, r in enumerate(rounds):
+        for i in r:
+            d[i] = t
+            for s_ in set(x for x in ops[i].srcs if x is not None and ops[x].kind != "const"):
+                uses[s_].append(t)
+                readers[s_].append((t, i))
+    outs = {v for v in prog.outputs.values() if ops[v].kind != "st"}
+    for v in outs:
+        uses[v].append(T)
+    vals = [v for v in d if ops[v].kind != "st"]
+    for v in vals:
+        uses[v].sort()
+
+    def lu(v):
+        return uses[v][-1] if uses[v] else d[v]
+    occ = [0] * (T + 1)
+    starts = defaultdict(list)     # phase -> values whose occupancy starts there (candidate scan)
+    for v in vals:
+        for t in range(max(d[v], 0), min(lu(v), T) + 1):
+            occ[t] += 1
+    origin = {}          # fill copy -> the original value (scratch owner)
+    scr_iv = {}          # original -> [first spill phase, last fill phase]
+    alive = set(vals)
+    nsp = nfi = 0
+    failed, last_ts = set(), None
+    while True:
+        ts = max(range(T), key=lambda t: occ[t])
+        if occ[ts] <= K:
+            break
+        if ts != last_ts:
+            failed, last_ts = set(), ts
+        best = None
+        for v in alive:
+            if v in failed or not (d[v] < ts < lu(v)):
+                continue
+            us = uses[v]
+            k = bisect.bisect_right(us, ts)
+            if k > 0 and us[k - 1] == ts:
+                continue
+            c = us[k]
+            a = us[k - 1] if k > 0 else d[v]
+            if d[v] == ts:
+                continue
+            need_spill = origin.get(v, v) not in scr_iv
+            # a side spill runs after its phase's ops: it may store a value defined in that phase
+            lo = max(a, d[v], 0) if need_spill else a + 1
+            if lo > ts - (1 if need_spill else 0) or (need_spill and c < lo + gap):
+                continue
+            if best is None or c > best[0]:
+                best = (c, v, a, need_spill, lo)
+        if best is None:
+            occv = [v for v in alive if max(d[v], 0) <= ts <= lu(v)]
+            cat = defaultdict(int)
+            for v in occv:
+                us = uses[v]
+                cat["read here" if ts in us else "def here" if d[v] == ts else "read next" if ts + 1 in us
+                    else "failed" if v in failed else "other"] += 1
+            raise RuntimeError("%s: cannot spill below %d slots at phase %d (%d occupied: %s)" % (
+                prog.name, K, ts, occ[ts], dict(cat)))
+        c, v, a, need_spill, lo = best
+        owner = origin.get(v, v)
+        end_old = a
+        ps = None
+        if need_spill:
+            ps = next((t for t in range(lo, ts) if side[t] < W), None)
+            if ps is None:
+                failed.add(v)
+                continue
+        low = max(ts + 1, ps + gap) if ps is not None else ts + 1
+        pf = next((t for t in range(min(c, T - 1), low - 1, -1) if side[t] < W), None)
+        if pf is None:
+            failed.add(v)
+            continue
+        if need_spill:
+            si = len(ops)
+            ops.append(Op("spill", srcs=(v,), imm=0))
+            ops[si].sec = "spill"
+            rounds[ps].append(si)
+            side[ps] += 1
+            d[si] = ps
+            bisect.insort(uses[v], ps)
+            readers[v].append((ps, si))
+            scr_iv[owner] = [ps, pf]
+            end_old = ps
+            nsp += 1
+        fi = len(ops)
+        ops.append(Op("fill", srcs=(), imm=0, deps=(owner,)))
+        ops[fi].sec = "fill"
+        rounds[pf].append(fi)
+        side[pf] += 1
+        nfi += 1
+        d[fi] = pf
+        origin[fi] = owner
+        scr_iv[owner][1] = max(scr_iv[owner][1], pf)
+        # reads of v from phase c on move to the fill
+        uses[fi] = [u for u in uses[v] if u >= c]
+        uses[v] = [u for u in uses[v] if u < c]
+        keep = []
+        for (t, i) in readers[v]:
+            if t >= c:
+                ops[i].srcs = tuple(fi if s_ == v else s_ for s_ in ops[i].srcs)
+                readers[fi].append((t, i))
+            else:
+                keep.append((t, i))
+        readers[v] = keep
+        if v in outs:
+            outs.discard(v)
+            outs.add(fi)
+            for name, o in prog.outputs.items():
+                if o == v:
+                    prog.outputs[name] = fi
+        for t in range(end_old + 1, pf):
+            occ[t] -= 1
+        alive.add(fi)
+        if lu(v) <= ts:
+            alive.discard(v)
+    # scratch entries: interval colouring of [first spill, last fill] per spilled value
+    iv = sorted((a, b, o) for o, (a, b) in scr_iv.items())
+    heap, nscr, entry = [], 0, {}
+    for a, b, o in iv:
+        if heap and heap[0][0] < a:
+            _, e = heapq.heappop(heap)
+        else:
+            e = nscr
+            nscr += 1
+        entry[o] = e
+        heapq.heappush(heap, (b, e))
+    for i in range(len(ops)):
+        if ops[i].kind == "spill":
+            ops[i].imm = entry[ops[i].srcs[0]]
+        elif ops[i].kind == "fill":
+            ops[i].imm = entry[origin[i]]
+    return nscr, nsp, nfi
