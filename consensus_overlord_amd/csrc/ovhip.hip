@@ -1969,6 +1969,9 @@ struct ovh_ctx {
   hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse; lazy)
   // ovh_verify_samemsg_device_async: [0], [1] the per-vote streams, in turn; [2] hash_to_G2 (lazy)
   hipStream_t vstream[3] = {};
+  // pipelined batches' per-vote stream pair (vote_pair; created with the context, before any
+  // lazily created stream, so each takes a hardware queue of its own)
+  hipStream_t pstream[2] = {};
   hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
@@ -2778,13 +2781,7 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
   // after the caller's work on `stream` and the slot's release (take_slot)
   hipStream_t vst = c->stream;
   if (pipe && c->vote_pair) {
-    for (int k = 0; k < 2; ++k)
-      if (!c->vstream[k]) {
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        HIPCHK(hipStreamCreateWithPriority(&c->vstream[k], hipStreamNonBlocking, hi));
-      }
-    vst = c->vstream[slot & 1];
+    vst = c->pstream[slot & 1];
     HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
     HIPCHK(hipStreamWaitEvent(vst, c->ev_front[slot], 0));
   }
@@ -3565,6 +3562,12 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
   if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e);
   if (const char* e = getenv("OVH_VOTE_PAIR")) c->vote_pair = atoi(e) != 0;
+  // A/B knobs of the pipelined pair: the pair's and the final streams'
+  // priorities (1: the pair high, the finals lowest -- r04r: 1,268k verifs/s; a normal-priority
+  // pair 1,256k, normal-priority finals 1,091k)
+  int pair_prio = 1, fin_prio = 1;
+  if (const char* e = getenv("OVH_PAIR_PRIO")) pair_prio = atoi(e);
+  if (const char* e = getenv("OVH_FINAL_LOW")) fin_prio = atoi(e);
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->wg_cap = 4u * (uint32_t)ncu;
@@ -3576,8 +3579,11 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
   bool ok = xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess &&
+            (!c->vote_pair ||
+             (hipStreamCreateWithPriority(&c->pstream[0], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess &&
+              hipStreamCreateWithPriority(&c->pstream[1], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess)) &&
             hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&
             hipMalloc(&c->vstart, 8) == hipSuccess && hipMemset(c->vstart, 0, 8) == hipSuccess &&
             hipMemset(c->result, 0, RES_WORDS * 4) == hipSuccess &&
@@ -3668,7 +3674,8 @@ int ovh_multi_peer_matrix(ovh_ctx* c, uint8_t* out, size_t cap) {
 static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2]})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
+                         c->pstream[0], c->pstream[1]})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
@@ -3697,7 +3704,8 @@ static void destroy_one(ovh_ctx* c) {
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2]})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
+                         c->pstream[0], c->pstream[1]})
     if (s) (void)hipStreamDestroy(s);
   delete c;
 }
