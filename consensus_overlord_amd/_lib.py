@@ -47,6 +47,7 @@ SIGNATURES = [
     ("ovh_batch_fallback_device", ctypes.c_int, [_vp, _sz, _vp]),
     ("ovh_verify_batch_device_async", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp]),
     ("ovh_verify_samemsg_device_async", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp]),
+    ("ovh_vote_spans", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_float), _sz]),
     ("ovh_verify_batch_async", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp, _vp]),
     ("ovh_batch_wait", ctypes.c_int, [_vp]),
     ("ovh_combine_partials_device_async", ctypes.c_int, [_vp, _sz, _vp, _sz, _vp, _vp]),

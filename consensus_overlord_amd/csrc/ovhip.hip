@@ -1966,6 +1966,10 @@ struct ovh_ctx {
   // Batches alternate between two final streams, so two finals may run at once (each shares a
   // SIMD with a vote wave and takes longer than a vote kernel there).
   hipStream_t fstream = nullptr, fstream2 = nullptr;
+  // OVH_NFIN=4: the batches' combined checks rotate over four final streams (A/B: with the
+  // pipelined pair 1,219k verifs/s against 1,266k on two, r04t)
+  hipStream_t fstream3 = nullptr, fstream4 = nullptr;
+  uint32_t nfin = 2;
   hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse; lazy)
   // ovh_verify_samemsg_device_async: [0], [1] the per-vote streams, in turn; [2] hash_to_G2 (lazy)
   hipStream_t vstream[3] = {};
@@ -2074,6 +2078,11 @@ struct ovh_ctx {
   std::vector<uint32_t> blind_h;  // host copy of the last compression blinds (upload_blinds)
   // OVH_FLAG_PROFILE: start/stop events per stage of the last batch call
   hipEvent_t ev0[OVH_NSTAGES] = {}, ev1[OVH_NSTAGES] = {};
+  // OVH_FLAG_PROFILE: start / end events of the last VEV_CAP batch vote kernels (ovh_vote_spans:
+  // pipelined vote grids overlap, so their device-level rate is the work over the union span)
+  static constexpr uint32_t VEV_CAP = 256;
+  hipEvent_t vev0[VEV_CAP] = {}, vev1[VEV_CAP] = {};
+  uint32_t vev_n = 0;
   uint32_t ev_mask = 0;
 };
 
@@ -2320,6 +2329,8 @@ static int sync_all(ovh_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->fstream));
   HIPCHK(hipStreamSynchronize(c->fstream2));
+  for (hipStream_t s : {c->fstream3, c->fstream4, c->pstream[0], c->pstream[1]})
+    if (s) HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
 
@@ -2423,7 +2434,8 @@ static int ensure_in(ovh_ctx* c, size_t bytes) {
 static int take_slot(ovh_ctx* c, int* slot) {
   const int k = (int)(c->pipe_k % OVH_BATCH_SLOTS);
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_back[k], 0));
-  c->fs[k] = (c->pipe_k & 1) ? c->fstream2 : c->fstream;
+  const uint32_t q = c->pipe_k % c->nfin;
+  c->fs[k] = q == 0 ? c->fstream : q == 1 ? c->fstream2 : q == 2 ? c->fstream3 : c->fstream4;
   ++c->pipe_k;
   c->last_slot = k;
   *slot = k;
@@ -2466,6 +2478,9 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
                        int32_t* d_codes, bool fold1 = true, bool alone = false, hipStream_t vst = nullptr) {
   Slab s{c->state_slot[slot], c->cap};
   hipStream_t st = vst ? vst : c->stream;
+  // with a per-vote stream of the pair: hash_to_field on `stream` (after the caller's work and
+  // the slot's release), the per-vote stream waits for it -- so the pair stream runs its vote
+  // kernels back to back
   c->ev_mask = 0;
   uint64_t seed, base;
   CHK(draw_seed(c, &seed, &base));
@@ -2478,9 +2493,16 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
   {  // hash_to_field on the main stream: its inputs are ready in that stream's order (the
      // staging copies, or a caller's writes on ovh_stream)
-    StageScope p(c, ST_H2F, st);
-    k_h2f<<<nblk(n), WG, 0, st>>>(n, d_hashes, c->xmd, s);
+    StageScope p(c, ST_H2F, c->stream);
+    k_h2f<<<nblk(n), WG, 0, c->stream>>>(n, d_hashes, c->xmd, s);
   }
+  if (st != c->stream) {
+    HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
+    HIPCHK(hipStreamWaitEvent(st, c->ev_front[slot], 0));
+  }
+  const bool vev = (c->flags & OVH_FLAG_PROFILE) != 0;
+  const uint32_t vk = c->vev_n % ovh_ctx::VEV_CAP;
+  if (vev) HIPCHK(hipEventRecord(c->vev0[vk], st));
   {
     StageScope p(c, ST_VOTE, st);
     if (key.bytes)
@@ -2492,6 +2514,10 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
     c->vlaunched += nwg;
     c->clk_wgs = nwg < VM_CLOCK_WGS ? nwg : VM_CLOCK_WGS;
     c->clk_table = key.bytes == nullptr;
+  }
+  if (vev) {
+    HIPCHK(hipEventRecord(c->vev1[vk], st));
+    ++c->vev_n;
   }
   if (fold1) {  // fold level 1: R0 -> R1 (one partial per 16-vote group)
     StageScope p(c, ST_FOLD, st);
@@ -2782,8 +2808,6 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
   hipStream_t vst = c->stream;
   if (pipe && c->vote_pair) {
     vst = c->pstream[slot & 1];
-    HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
-    HIPCHK(hipStreamWaitEvent(vst, c->ev_front[slot], 0));
   }
   CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, !side, true, vst));
   hipStream_t fst = c->fs[slot];
@@ -3568,6 +3592,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   int pair_prio = 1, fin_prio = 1;
   if (const char* e = getenv("OVH_PAIR_PRIO")) pair_prio = atoi(e);
   if (const char* e = getenv("OVH_FINAL_LOW")) fin_prio = atoi(e);
+  if (const char* e = getenv("OVH_NFIN")) c->nfin = atoi(e) >= 4 ? 4 : 2;
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
     c->wg_cap = 4u * (uint32_t)ncu;
@@ -3581,6 +3606,9 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess &&
+            (c->nfin < 4 ||
+             (hipStreamCreateWithPriority(&c->fstream3, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess &&
+              hipStreamCreateWithPriority(&c->fstream4, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess)) &&
             (!c->vote_pair ||
              (hipStreamCreateWithPriority(&c->pstream[0], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess &&
               hipStreamCreateWithPriority(&c->pstream[1], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess)) &&
@@ -3598,9 +3626,12 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   for (int k = 0; ok && k < 4; ++k) ok = hipEventCreateWithFlags(&c->ev_x[k], hipEventDisableTiming) == hipSuccess;
   for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k)
     for (int q = 0; ok && q < 4; ++q) ok = hipEventCreateWithFlags(&c->ev_m[k][q], hipEventDisableTiming) == hipSuccess;
-  if (ok && (flags & OVH_FLAG_PROFILE))
+  if (ok && (flags & OVH_FLAG_PROFILE)) {
     for (int k = 0; ok && k < OVH_NSTAGES; ++k)
       ok = hipEventCreate(&c->ev0[k]) == hipSuccess && hipEventCreate(&c->ev1[k]) == hipSuccess;
+    for (uint32_t k = 0; ok && k < ovh_ctx::VEV_CAP; ++k)
+      ok = hipEventCreate(&c->vev0[k]) == hipSuccess && hipEventCreate(&c->vev1[k]) == hipSuccess;
+  }
   if (!ok) {
     destroy_one(c);
     return nullptr;
@@ -3674,7 +3705,7 @@ int ovh_multi_peer_matrix(ovh_ctx* c, uint8_t* out, size_t cap) {
 static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
+  for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->fstream4, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
                          c->pstream[0], c->pstream[1]})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
@@ -3703,8 +3734,12 @@ static void destroy_one(ovh_ctx* c) {
     if (c->ev0[k]) (void)hipEventDestroy(c->ev0[k]);
     if (c->ev1[k]) (void)hipEventDestroy(c->ev1[k]);
   }
+  for (uint32_t k = 0; k < ovh_ctx::VEV_CAP; ++k) {
+    if (c->vev0[k]) (void)hipEventDestroy(c->vev0[k]);
+    if (c->vev1[k]) (void)hipEventDestroy(c->vev1[k]);
+  }
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
+  for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->fstream4, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
                          c->pstream[0], c->pstream[1]})
     if (s) (void)hipStreamDestroy(s);
   delete c;
@@ -3726,7 +3761,7 @@ int ovh_device_count(ovh_ctx* c) { return !c ? 0 : c->sub.empty() ? 1 : (int)c->
 // the main and the side stream (streams = 2: two launches co-resident when the LDS allows: two
 // waves per SIMD). *ms = the wall time of the whole sequence (HIP events).
 int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams, float* ms) {
-  if (!c || !ms || n == 0 || n > (1u << 20) || reps < 1 || streams < 1 || streams > 2 || prog < 0 || prog > 1)
+  if (!c || !ms || n == 0 || n > (1u << 20) || reps < 1 || streams < 1 || streams > 4 || prog < 0 || prog > 1)
     return OVH_ERR_ARG;
   if (!c->sub.empty()) c = c->sub[0];
   std::lock_guard<std::mutex> g(c->mu);
@@ -3745,8 +3780,12 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
   HIPCHK(hipEventCreate(&e1));
   HIPCHK(hipEventRecord(e0, c->stream));
   HIPCHK(hipStreamWaitEvent(c->xstream, e0, 0));
+  for (hipStream_t p : c->pstream)
+    if (p) HIPCHK(hipStreamWaitEvent(p, e0, 0));
   for (int r = 0; r < reps; ++r) {
-    const hipStream_t st = (streams == 2 && (r & 1)) ? c->xstream : c->stream;
+    // streams 3: every launch on pipelined pair stream 0; 4: the pair in turn
+    hipStream_t st = (streams == 2 && (r & 1)) ? c->xstream : c->stream;
+    if (streams >= 3 && c->pstream[0]) st = c->pstream[streams == 4 ? (r & 1) : 0];
     if (prog == 0)
       k_vm_vsame<false><<<(N + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(N, 0, c->vm_vsame, c->vm_consts,
                                                                                c->in_buf + n * 96, PkSrc{}, c->in_buf,
@@ -3759,6 +3798,11 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e1, c->xstream));
   HIPCHK(hipStreamWaitEvent(c->stream, e1, 0));
+  for (hipStream_t p : c->pstream)
+    if (p) {
+      HIPCHK(hipEventRecord(e1, p));
+      HIPCHK(hipStreamWaitEvent(c->stream, e1, 0));
+    }
   HIPCHK(hipEventRecord(e1, c->stream));
   HIPCHK(hipEventSynchronize(e1));
   HIPCHK(hipEventElapsedTime(ms, e0, e1));
@@ -3805,6 +3849,28 @@ int ovh_stage_times(ovh_ctx* c, float* ms, size_t max) {
       if (hipEventElapsedTime(&ms[k], c->ev0[k], c->ev1[k]) != hipSuccess) return -OVH_ERR_DEVICE;
   }
   return (int)n;
+}
+
+int ovh_vote_spans(ovh_ctx* c, float* ms, size_t max) {
+  if (!c || (!ms && max)) return -OVH_ERR_ARG;
+  if (!c->sub.empty()) c = c->sub[0];
+  if (!(c->flags & OVH_FLAG_PROFILE)) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (max == 0) {  // reset
+    c->vev_n = 0;
+    return 0;
+  }
+  if (hipSetDevice(c->device) != hipSuccess || sync_all(c)) return -OVH_ERR_DEVICE;
+  const uint32_t n = c->vev_n < ovh_ctx::VEV_CAP ? c->vev_n : ovh_ctx::VEV_CAP;
+  const uint32_t first = c->vev_n - n;  // the oldest kept batch
+  size_t k = 0;
+  for (uint32_t j = 0; j < n && 2 * k + 1 < max; ++j, ++k) {
+    const uint32_t e = (first + j) % ovh_ctx::VEV_CAP, e0 = first % ovh_ctx::VEV_CAP;
+    if (hipEventElapsedTime(&ms[2 * k], c->vev0[e0], c->vev0[e]) != hipSuccess ||
+        hipEventElapsedTime(&ms[2 * k + 1], c->vev0[e0], c->vev1[e]) != hipSuccess)
+      return -OVH_ERR_DEVICE;
+  }
+  return (int)k;
 }
 
 const char* ovh_stage_name(int k) { return (k >= 0 && k < OVH_NSTAGES) ? STAGE_NAMES[k] : nullptr; }
@@ -4742,11 +4808,14 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   // are read in ovh_stream order (include/ovhip.h): waiting on `stream` here would also wait for
   // the previous batch's gather and combine queued there and serialise the pipeline (r03b: 1,062k
   // -> 796k verifs/s at one rank).
-  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false));
+  // the vote kernels of consecutive shards on the per-vote stream pair (vote_pair), as in
+  // ovh_verify_batch_device_async
+  hipStream_t vst = c->vote_pair ? c->pstream[slot & 1] : nullptr;
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false, false, vst));
   hipStream_t fst = c->fs[slot];
   int reg;
   uint32_t m;
-  CHK(side_front(c, slot, (uint32_t)n, true, 1, &reg, &m));
+  CHK(side_front(c, slot, (uint32_t)n, true, 1, &reg, &m, vst));
   CHK(enqueue_msm(c, fst, slot, (uint32_t)n, d_codes));
   HIPCHK(hipEventRecord(c->ev_x[0], st));  // the caller's earlier work (a gather out of d_partial)
   HIPCHK(hipStreamWaitEvent(fst, c->ev_x[0], 0));

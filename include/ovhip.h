@@ -254,6 +254,12 @@ int ovh_combine_partials_device_async(ovh_ctx* ctx, size_t k, const uint8_t* d_p
  * and returns that count (0 without the flag, <0 on error). */
 int ovh_stage_times(ovh_ctx* ctx, float* ms, size_t max);
 const char* ovh_stage_name(int stage);
+/* Diagnostics (context created with OVH_FLAG_PROFILE): (start, end) in ms, relative to the
+ * first, of the vote kernels of the last batches (up to 256, oldest first) -- pipelined vote
+ * grids of consecutive batches overlap, so their device-level rate is the work over the union of
+ * these spans. Writes min(count, max / 2) pairs and returns that number; max = 0 forgets the
+ * batches recorded so far. */
+int ovh_vote_spans(ovh_ctx* ctx, float* ms, size_t max);
 
 /* Diagnostics (context created with OVH_FLAG_VM_TRACE): the wall clock (100 MHz counter) of
  * workgroup 0 of the last launch of VM program `prog` (0 vote, 1 fold, 2 final, 3 vote_t)
@@ -262,7 +268,8 @@ const char* ovh_stage_name(int stage);
 int ovh_vm_trace(ovh_ctx* ctx, int prog, uint64_t* stamps, size_t max);
 /* Diagnostics: occupancy A/B of a VM program -- `reps` launches of program `prog` (0 vsame, 1
  * vote) over n votes, on one stream (streams = 1) or alternating over two (streams = 2: two
- * launches co-resident when the LDS allows, i.e. two waves per SIMD). *ms = wall time. */
+ * launches co-resident when the LDS allows, i.e. two waves per SIMD); streams = 3: every launch
+ * on the pipelined pair's first stream, 4: alternating over the pair. *ms = wall time. */
 int ovh_diag_vm_occupancy(ovh_ctx* ctx, int prog, size_t n, int reps, int streams, float* ms);
 /* Diagnostics (context created with OVH_FLAG_VM_CLOCK): per workgroup of the last vote / vote_t
  * launch, (delta s_memtime, delta s_memrealtime) around its VM program -- shader cycles and

@@ -22,7 +22,7 @@ def main():
     ms = ctypes.c_float()
     out = {}
     for prog, name in ((0, "vsame"), (1, "vote")):
-        for streams in (1, 2, 1, 2):
+        for streams in ((1, 2, 3, 4, 1, 2, 3, 4) if prog else (1, 2, 1, 2)):
             assert c.lib.ovh_diag_vm_occupancy(c.ptr, prog, 4096, 8, streams, ctypes.byref(ms)) == 0
             out.setdefault("%s_streams%d_ms_per_launch" % (name, streams), []).append(round(ms.value / 8, 4))
     for k in list(out):
