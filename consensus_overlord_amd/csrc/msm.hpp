@@ -8,8 +8,8 @@
 // digit d = byte w of its scalar lands in bucket w * 255 + d - 1 (d = 0: nothing).
 //
 //   k_msm_count    lane per vote: bucket histogram in LDS, then one global add per bucket
-//   k_msm_scan     one workgroup: bucket offsets, and per tree level the prefix of the
-//                  bucket's pair counts (the level kernels' work lists) -- all in LDS
+//   k_msm_scan     one wave: bucket offsets, and per tree level the prefix of the bucket's
+//                  pair counts (the level kernels' work lists)
 //   k_msm_scatter  lane per vote: point ids into their bucket's range (counting sort)
 //   k_msm_pair     the VM pair kernels (8- or 16-lane slices, Fp-VM slots in LDS hold the
 //                  bucket accumulators): bucket tree level 0 (madd, affine points), levels >= 1
@@ -39,12 +39,22 @@ struct MsmArgs {
 
 __device__ __forceinline__ uint32_t msm_half(uint64_t r, uint32_t h) { return h ? (uint32_t)(r >> 32) : (uint32_t)r; }
 
-__global__ __launch_bounds__(256) void k_msm_count(uint32_t n, uint64_t seed, uint64_t base,
-                                                   const int32_t* __restrict__ codes, uint32_t* __restrict__ cnt) {
+// One-wave workgroups: beside two co-resident vote grids (two waves per SIMD everywhere) a
+// workgroup of four or sixteen waves waits until that many slots free up on one CU -- r04w trace:
+// the 256-thread count kernel averaged 0.59 ms and peaked at 8.7 ms there, holding up the final.
+#define MSM_TPB 64
+
+__global__ __launch_bounds__(MSM_TPB) void k_msm_zero(uint32_t* __restrict__ cnt) {
+  const uint32_t k = blockIdx.x * MSM_TPB + threadIdx.x;
+  if (k < MSM_NB) cnt[k] = 0;
+}
+
+__global__ __launch_bounds__(MSM_TPB) void k_msm_count(uint32_t n, uint64_t seed, uint64_t base,
+                                                       const int32_t* __restrict__ codes, uint32_t* __restrict__ cnt) {
   __shared__ uint32_t h[MSM_NB];
-  for (uint32_t k = threadIdx.x; k < MSM_NB; k += 256) h[k] = 0;
+  for (uint32_t k = threadIdx.x; k < MSM_NB; k += MSM_TPB) h[k] = 0;
   __syncthreads();
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t i = blockIdx.x * MSM_TPB + threadIdx.x;
   if (i < n && codes[i] == 0) {  // failed votes contribute the identity
     const uint64_t r = vote_scalar(seed, base, i);
     for (uint32_t hh = 0; hh < 2; ++hh) {
@@ -56,55 +66,68 @@ __global__ __launch_bounds__(256) void k_msm_count(uint32_t n, uint64_t seed, ui
     }
   }
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < MSM_NB; k += 256)
+  for (uint32_t k = threadIdx.x; k < MSM_NB; k += MSM_TPB)
     if (h[k]) atomicAdd(&cnt[k], h[k]);
 }
 
-// exclusive prefix over the 1024 threads of the workgroup (thread t holds v); *total = sum
-__device__ __forceinline__ uint32_t block_scan_1024(uint32_t v, uint32_t* s, uint32_t* total) {
+// Exclusive prefix over the MSM_NB values v(b) of one wave: lane t owns the 16 consecutive
+// entries 16 t .. 16 t + 15 (MSM_NB <= 1024), scans them serially, and the lanes' sums are
+// scanned across the wave (shuffles). out(b) = the prefix; returns the total (every lane).
+template <class F, class G>
+__device__ __forceinline__ uint32_t wave_scan_nb(F v, G out) {
+  static_assert(MSM_NB <= 16 * 64, "16 entries per lane");
   const uint32_t t = threadIdx.x;
-  s[t] = v;
-  __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {
-    const uint32_t x = t >= d ? s[t - d] : 0;
-    __syncthreads();
-    s[t] += x;
-    __syncthreads();
+  uint32_t loc[16], sum = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t b = 16 * t + j;
+    loc[j] = b < MSM_NB ? v(b) : 0u;
+    sum += loc[j];
   }
-  const uint32_t incl = s[t];
-  *total = s[1023];
-  __syncthreads();
-  return incl - v;
+  uint32_t incl = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t x = __shfl_up(incl, d, 64);
+    if (t >= (uint32_t)d) incl += x;
+  }
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t b = 16 * t + j;
+    if (b < MSM_NB) out(b, run);
+    run += loc[j];
+  }
+  return __shfl(incl, 63, 64);
 }
 
-__global__ __launch_bounds__(1024) void k_msm_scan(uint32_t nlev, const uint32_t* __restrict__ cnt,
-                                                   uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
-                                                   uint32_t* __restrict__ pf) {
-  __shared__ uint32_t s[1024];
-  const uint32_t b = threadIdx.x;
-  const uint32_t c = b < MSM_NB ? cnt[b] : 0;
-  uint32_t tot;
-  const uint32_t ex = block_scan_1024(c, s, &tot);
-  if (b < MSM_NB) {
-    off[b] = ex;
-    cur[b] = ex;
-  }
-  if (b == 0) off[MSM_NB] = tot;
+__global__ __launch_bounds__(64) void k_msm_scan(uint32_t nlev, const uint32_t* __restrict__ cnt,
+                                                 uint32_t* __restrict__ off, uint32_t* __restrict__ cur,
+                                                 uint32_t* __restrict__ pf) {
+  const uint32_t tot = wave_scan_nb([&](uint32_t b) { return cnt[b]; },
+                                    [&](uint32_t b, uint32_t e) {
+                                      off[b] = e;
+                                      cur[b] = e;
+                                    });
+  if (threadIdx.x == 0) off[MSM_NB] = tot;
   for (uint32_t lv = 0; lv < nlev; ++lv) {
     // level 0: every even entry (its pair, or alone at a bucket's odd end); level l: entries
     // k = j 2^(l+1) whose partner k + 2^l exists
     const uint32_t h = 1u << lv;
-    const uint32_t pc = lv == 0 ? (c + 1) / 2 : (c > h ? (c - h + 2 * h - 1) >> (lv + 1) : 0);
-    const uint32_t e = block_scan_1024(pc, s, &tot);
-    if (b < MSM_NB) pf[(size_t)lv * (MSM_NB + 1) + b] = e;
-    if (b == 0) pf[(size_t)lv * (MSM_NB + 1) + MSM_NB] = tot;
+    uint32_t* p = pf + (size_t)lv * (MSM_NB + 1);
+    const uint32_t t = wave_scan_nb(
+        [&](uint32_t b) {
+          const uint32_t c = cnt[b];
+          return lv == 0 ? (c + 1) / 2 : (c > h ? (c - h + 2 * h - 1) >> (lv + 1) : 0u);
+        },
+        [&](uint32_t b, uint32_t e) { p[b] = e; });
+    if (threadIdx.x == 0) p[MSM_NB] = t;
   }
 }
 
-__global__ __launch_bounds__(256) void k_msm_scatter(uint32_t n, uint64_t seed, uint64_t base,
-                                                     const int32_t* __restrict__ codes, uint32_t* __restrict__ cur,
-                                                     uint32_t* __restrict__ ent) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(MSM_TPB) void k_msm_scatter(uint32_t n, uint64_t seed, uint64_t base,
+                                                         const int32_t* __restrict__ codes, uint32_t* __restrict__ cur,
+                                                         uint32_t* __restrict__ ent) {
+  const uint32_t i = blockIdx.x * MSM_TPB + threadIdx.x;
   if (i >= n || codes[i] != 0) return;
   const uint64_t r = vote_scalar(seed, base, i);
   for (uint32_t hh = 0; hh < 2; ++hh) {

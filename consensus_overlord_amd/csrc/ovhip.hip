@@ -2583,11 +2583,11 @@ static int enqueue_msm(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, const i
   uint32_t nlev = 1;  // tree levels: 2^nlev >= the largest possible bucket (2n points)
   while ((1ull << nlev) < 2ull * n) ++nlev;
   if (nlev > MSM_LV) return OVH_ERR_ARG;
-  HIPCHK(hipMemsetAsync((void*)a.cnt, 0, MSM_NB * 4, st));
-  const uint32_t nb = (n + 255) / 256;
-  k_msm_count<<<nb, 256, 0, st>>>(n, seed, base, d_codes, (uint32_t*)a.cnt);
-  k_msm_scan<<<1, 1024, 0, st>>>(nlev, a.cnt, (uint32_t*)a.off, cur, (uint32_t*)a.pf);
-  k_msm_scatter<<<nb, 256, 0, st>>>(n, seed, base, d_codes, cur, (uint32_t*)a.ent);
+  k_msm_zero<<<(MSM_NB + MSM_TPB - 1) / MSM_TPB, MSM_TPB, 0, st>>>((uint32_t*)a.cnt);  // (one-wave workgroups)
+  const uint32_t nb = (n + MSM_TPB - 1) / MSM_TPB;
+  k_msm_count<<<nb, MSM_TPB, 0, st>>>(n, seed, base, d_codes, (uint32_t*)a.cnt);
+  k_msm_scan<<<1, 64, 0, st>>>(nlev, a.cnt, (uint32_t*)a.off, cur, (uint32_t*)a.pf);
+  k_msm_scatter<<<nb, MSM_TPB, 0, st>>>(n, seed, base, d_codes, cur, (uint32_t*)a.ent);
   constexpr uint32_t SL8 = 64 / VM_MADD_W, SL16 = 64 / VM_HDBL1_W;
   auto grid = [](uint64_t pairs, uint32_t sl) { return (uint32_t)((pairs + sl - 1) / sl); };
   // bucket trees: level 0 pairs (<= 4n + NB), level l (<= 8n / 2^(l+1) + NB), in place
