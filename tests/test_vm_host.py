@@ -293,3 +293,34 @@ def test_samemsg_programs_on_interpreter(hx, built, golden_votes, any_all):  # n
     fin = dict(zip(progs.GFIN_IN, [1] + [0] * 11 + [o["st:r%d" % j] for j in range(3)] +
                    [h["st:h%d" % j] for j in range(6)] + gen._proj(rs)))
     assert run("gfin", fin) == {"ok": 1}
+
+
+def test_spill_pass_bounds_slots_and_keeps_values(hx, built, golden_votes):  # noqa: F811
+    """sched.spill_pass on the vote program at K = 120 (gen.py builds it at 90; 159 slots
+    unspilled): at most K slots, every fill at least `gap` (3) phases after its value's spill,
+    the schedule's phases unchanged, and the outputs (simulator, and the interpreter with side
+    words) equal the unspilled program's on the golden votes."""
+    consts, progs_ = built
+    _, vsc, vwords, _, _ = progs_["vote"]
+    K = 120
+    builder, _, _ = progs.PROGRAMS["vote"]
+    prog = builder()
+    prog.fuse()
+    sc = sched.schedule(prog, gen.WIDTH["vote"], consts, max_slots=400, heavy_w=gen.HEAVY_W["vote"],
+                        hoist=gen.HOIST["vote"], stretch=gen.STRETCH["vote"], mixed=False, spill_k=K)
+    words = sched.encode(sc)
+    assert sc.nslots <= K and sc.nscr > 0 and sc.nfill >= sc.nspill > 0 and sc.nrounds == vsc.nrounds
+    spill_at, fill_at = {}, []
+    for t, rr in enumerate(sc.rounds):
+        for i in rr:
+            if prog.ops[i].kind == "spill":
+                spill_at[prog.ops[i].srcs[0]] = t
+            elif prog.ops[i].kind == "fill":
+                fill_at.append((t, prog.ops[i].deps[0]))
+    assert all(t >= spill_at[o] + 3 for t, o in fill_at)
+    r = 0x0F1E2D3C4B5A6978
+    for k, inp in enumerate(golden_votes):
+        ref = sched.simulate(vsc, vwords, inp, r)
+        sim = sched.simulate(sc, words, inp, r)
+        assert sim == ref
+        assert_same(run_vm(hx, consts, sc, words, inp, r, 0), sim, "vote %d spilled to %d" % (k, K))
