@@ -1975,7 +1975,8 @@ struct ovh_ctx {
   hipStream_t vstream[3] = {};
   // pipelined batches' per-vote stream pair (vote_pair; created with the context, before any
   // lazily created stream, so each takes a hardware queue of its own)
-  hipStream_t pstream[2] = {};
+  hipStream_t pstream[3] = {};
+  uint32_t npair = 2;  // OVH_VOTE_PAIR=3: three per-vote streams in turn (A/B)
   hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
@@ -2329,7 +2330,7 @@ static int sync_all(ovh_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->fstream));
   HIPCHK(hipStreamSynchronize(c->fstream2));
-  for (hipStream_t s : {c->fstream3, c->fstream4, c->pstream[0], c->pstream[1]})
+  for (hipStream_t s : {c->fstream3, c->fstream4, c->pstream[0], c->pstream[1], c->pstream[2]})
     if (s) HIPCHK(hipStreamSynchronize(s));
   return 0;
 }
@@ -2807,7 +2808,7 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
   // after the caller's work on `stream` and the slot's release (take_slot)
   hipStream_t vst = c->stream;
   if (pipe && c->vote_pair) {
-    vst = c->pstream[slot & 1];
+    vst = c->pstream[slot % c->npair];
   }
   CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, !side, true, vst));
   hipStream_t fst = c->fs[slot];
@@ -3585,7 +3586,10 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   if (const char* e = getenv("OVH_FOLD_SIDE")) c->fold_side = atoi(e) != 0;
   if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
   if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e);
-  if (const char* e = getenv("OVH_VOTE_PAIR")) c->vote_pair = atoi(e) != 0;
+  if (const char* e = getenv("OVH_VOTE_PAIR")) {
+    c->vote_pair = atoi(e) != 0;
+    c->npair = atoi(e) >= 3 ? 3 : 2;
+  }
   // A/B knobs of the pipelined pair: the pair's and the final streams'
   // priorities (1: the pair high, the finals lowest -- r04r: 1,268k verifs/s; a normal-priority
   // pair 1,256k, normal-priority finals 1,091k)
@@ -3611,7 +3615,9 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
               hipStreamCreateWithPriority(&c->fstream4, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess)) &&
             (!c->vote_pair ||
              (hipStreamCreateWithPriority(&c->pstream[0], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess &&
-              hipStreamCreateWithPriority(&c->pstream[1], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess)) &&
+              hipStreamCreateWithPriority(&c->pstream[1], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess &&
+              (c->npair < 3 ||
+               hipStreamCreateWithPriority(&c->pstream[2], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess))) &&
             hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&
             hipMalloc(&c->vstart, 8) == hipSuccess && hipMemset(c->vstart, 0, 8) == hipSuccess &&
             hipMemset(c->result, 0, RES_WORDS * 4) == hipSuccess &&
@@ -3706,7 +3712,7 @@ static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->fstream4, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
-                         c->pstream[0], c->pstream[1]})
+                         c->pstream[0], c->pstream[1], c->pstream[2]})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
@@ -3740,7 +3746,7 @@ static void destroy_one(ovh_ctx* c) {
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->fstream4, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
-                         c->pstream[0], c->pstream[1]})
+                         c->pstream[0], c->pstream[1], c->pstream[2]})
     if (s) (void)hipStreamDestroy(s);
   delete c;
 }
@@ -3775,6 +3781,7 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
   const Slab s{c->state_slot[0], c->cap};
   int32_t* dc = (int32_t*)(c->in_buf + n * 144);
   const uint32_t N = (uint32_t)n;
+  const bool scr_alt = getenv("OVH_DIAG_SCR_ALT") && atoi(getenv("OVH_DIAG_SCR_ALT")) != 0;
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
@@ -3783,7 +3790,8 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
   for (hipStream_t p : c->pstream)
     if (p) HIPCHK(hipStreamWaitEvent(p, e0, 0));
   for (int r = 0; r < reps; ++r) {
-    // streams 3: every launch on pipelined pair stream 0; 4: the pair in turn
+    // streams 3: every launch on pipelined pair stream 0; 4: the pair in turn; prog 1 with
+    // OVH_DIAG_SCR_ALT=1: consecutive launches use two slots' scratch (as two batches do)
     hipStream_t st = (streams == 2 && (r & 1)) ? c->xstream : c->stream;
     if (streams >= 3 && c->pstream[0]) st = c->pstream[streams == 4 ? (r & 1) : 0];
     if (prog == 0)
@@ -3793,7 +3801,8 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
     else
       k_vm_vote<<<(N + VM_SLICES - 1) / VM_SLICES, 64, LDS_VOTE, st>>>(N, c->vm_vote, c->vm_fold, c->vm_consts,
                                                                       c->in_buf + n * 96, c->in_buf, s, 1, 0, dc,
-                                                                      region_F(c, 0, 0), nullptr, c->vscr[0]);
+                                                                      region_F(c, 0, 0), nullptr,
+                                                                      c->vscr[scr_alt ? (r & 1) : 0]);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(e1, c->xstream));
@@ -4810,7 +4819,7 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   // -> 796k verifs/s at one rank).
   // the vote kernels of consecutive shards on the per-vote stream pair (vote_pair), as in
   // ovh_verify_batch_device_async
-  hipStream_t vst = c->vote_pair ? c->pstream[slot & 1] : nullptr;
+  hipStream_t vst = c->vote_pair ? c->pstream[slot % c->npair] : nullptr;
   CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false, false, vst));
   hipStream_t fst = c->fs[slot];
   int reg;
