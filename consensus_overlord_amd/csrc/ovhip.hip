@@ -3018,13 +3018,17 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   const hipStream_t fst = c->fs[slot];
   hipStream_t st = c->stream;
   if (one) {
-    for (hipStream_t& v : c->vstream)
-      if (!v) {  // high priority: that pool's hardware queues hold only these three streams
+    // high priority: that pool's four hardware queues hold only these three streams -- the
+    // batch path's per-vote pair when the context has it (a fourth and fifth high-priority
+    // stream shared queue 8 with the hash_to_G2 stream and serialised vsame behind it, r04ab)
+    hipStream_t* pair = c->pstream[0] ? c->pstream : c->vstream;
+    for (hipStream_t* v : {&pair[0], &pair[1]})
+      if (!*v) {
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        HIPCHK(hipStreamCreateWithPriority(&v, hipStreamNonBlocking, hi));
+        HIPCHK(hipStreamCreateWithPriority(v, hipStreamNonBlocking, hi));
       }
-    st = c->vstream[c->pipe_k & 1];
+    st = pair[c->pipe_k & 1];
   }
   // hash_to_G2 per hash beside the per-vote programs at normal priority (at the final streams'
   // low priority it took 2.8 ms beside 1,024 vsame waves, r04g): on the side stream for a staged
@@ -3034,8 +3038,8 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   // queues and serialised them (r04m trace), and on ovh_stream it delayed the next batch's
   // per-vote work (r04n), so the one-hash path runs on three high-priority streams (a pool of
   // their own: the two per-vote streams and this one) and the final streams (its key sums there).
-  if (!one && !c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-  const hipStream_t xs = one ? fst : c->xstream, hs = one ? c->vstream[2] : c->xstream;
+  if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+  const hipStream_t xs = one ? fst : c->xstream, hs = c->xstream;
   HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));  // the inputs (and the slot free: take_slot)
   HIPCHK(hipStreamWaitEvent(hs, c->ev_front[slot], 0));
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
