@@ -1976,7 +1976,7 @@ struct ovh_ctx {
   // pipelined batches' per-vote stream pair (vote_pair; created with the context, before any
   // lazily created stream, so each takes a hardware queue of its own)
   hipStream_t pstream[3] = {};
-  uint32_t npair = 2;  // OVH_VOTE_PAIR=3: three per-vote streams in turn (A/B)
+  uint32_t npair = 2;  // OVH_VOTE_PAIR=3: three per-vote streams in turn, =1: one (A/B)
   hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
@@ -3592,7 +3592,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e);
   if (const char* e = getenv("OVH_VOTE_PAIR")) {
     c->vote_pair = atoi(e) != 0;
-    c->npair = atoi(e) >= 3 ? 3 : 2;
+    c->npair = atoi(e) >= 3 ? 3 : atoi(e) == 1 ? 1 : 2;
   }
   // A/B knobs of the pipelined pair: the pair's and the final streams'
   // priorities (1: the pair high, the finals lowest -- r04r: 1,268k verifs/s; a normal-priority
