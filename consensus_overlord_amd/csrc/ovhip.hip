@@ -3780,7 +3780,10 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
   CHK(ensure_in(c, n * 176 + 64));
   CHK(sync_all(c));
   if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-  HIPCHK(hipMemsetAsync(c->in_buf, 0, n * 176, c->stream));
+  // OVH_DIAG_KEEP_IN=1: keep the staged votes of a preceding ovh_verify_batch (real data: the
+  // VM's timing does not depend on it, its power draw may)
+  if (!(getenv("OVH_DIAG_KEEP_IN") && atoi(getenv("OVH_DIAG_KEEP_IN")) != 0))
+    HIPCHK(hipMemsetAsync(c->in_buf, 0, n * 176, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   const Slab s{c->state_slot[0], c->cap};
   int32_t* dc = (int32_t*)(c->in_buf + n * 144);
