@@ -411,7 +411,9 @@ def vote_clock(sigs, hs, pks, seconds: float):
     c.close()
     if not len(ghz):
         return None
+    wg_ms = np.sort(st[:, 1]) * 1e-5     # s_memrealtime ticks at 100 MHz -> ms
     return {"clock_ghz": round(float(np.median(ghz)), 3),
+            "wg_ms_median": round(float(np.median(wg_ms)), 4),
             "p10_p90_ghz": [round(float(ghz[len(ghz) // 10]), 3), round(float(ghz[len(ghz) * 9 // 10]), 3)],
             "workgroups": int(len(ghz)), "batches": k, "seconds": round(time.perf_counter() - t0, 2),
             "basis": "median over the last vote launch's workgroups of delta s_memtime / delta s_memrealtime "

@@ -3812,6 +3812,11 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
                                                                       c->vscr[scr_alt ? (r & 1) : 0]);
   }
   HIPCHK(hipGetLastError());
+  if (prog == 1) {  // OVH_FLAG_VM_CLOCK: ovh_vm_clock reads the launches' per-workgroup stamps
+    const uint32_t nwg = (N + VM_SLICES - 1) / VM_SLICES;
+    c->clk_wgs = nwg < VM_CLOCK_WGS ? nwg : VM_CLOCK_WGS;
+    c->clk_table = false;
+  }
   HIPCHK(hipEventRecord(e1, c->xstream));
   HIPCHK(hipStreamWaitEvent(c->stream, e1, 0));
   for (hipStream_t p : c->pstream)
