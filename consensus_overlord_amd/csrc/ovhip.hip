@@ -3610,16 +3610,38 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   }
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
+  // OVH_FIN_CUS=N (A/B): the final streams on N CUs spread over the device (CU mask), and with
+  // OVH_VOTE_EXCL=1 the per-vote pair on the others -- the final-stream kernels then take LDS
+  // only where no vote grid needs it
+  int fin_cus = 0, vote_excl = 0;
+  if (const char* e = getenv("OVH_FIN_CUS")) fin_cus = atoi(e);
+  if (const char* e = getenv("OVH_VOTE_EXCL")) vote_excl = atoi(e);
+  std::vector<uint32_t> fmask, vmask;
+  if (fin_cus > 0 && ncu > fin_cus) {
+    fmask.assign(((size_t)ncu + 31) / 32, 0u);
+    vmask.assign(fmask.size(), 0u);
+    for (int k = 0; k < ncu; ++k) vmask[k / 32] |= 1u << (k % 32);
+    const int step = ncu / fin_cus;
+    for (int j = 0; j < fin_cus; ++j) {
+      const int k = j * step;
+      fmask[k / 32] |= 1u << (k % 32);
+      vmask[k / 32] &= ~(1u << (k % 32));
+    }
+  }
+  auto mk = [&](hipStream_t* st, int prio, const std::vector<uint32_t>& mask) {
+    if (!mask.empty()) return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()) == hipSuccess;
+    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio) == hipSuccess;
+  };
+  const std::vector<uint32_t> none;
+  const std::vector<uint32_t>& pmask = vote_excl ? vmask : none;
   bool ok = xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess &&
+            mk(&c->fstream, fin_prio ? lo : 0, fmask) && mk(&c->fstream2, fin_prio ? lo : 0, fmask) &&
             (c->nfin < 4 ||
              (hipStreamCreateWithPriority(&c->fstream3, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess &&
               hipStreamCreateWithPriority(&c->fstream4, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess)) &&
             (!c->vote_pair ||
-             (hipStreamCreateWithPriority(&c->pstream[0], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess &&
-              hipStreamCreateWithPriority(&c->pstream[1], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess &&
+             (mk(&c->pstream[0], pair_prio ? hi : 0, pmask) && mk(&c->pstream[1], pair_prio ? hi : 0, pmask) &&
               (c->npair < 3 ||
                hipStreamCreateWithPriority(&c->pstream[2], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess))) &&
             hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&
