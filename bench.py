@@ -553,6 +553,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.steps):
         step(args.warmup + s)
+    enqueue_s = time.perf_counter() - t0     # host time to enqueue the K batches (diagnostic)
     wait_all()
     torch.cuda.synchronize()
     if world > 1:
@@ -695,6 +696,7 @@ def main():
             },
             "stage_ms": stages,
             "batch_latency_ms": round(float(np.median(lat)) * 1e3, 3) if lat else None,
+            "enqueue_ms_per_step": round(enqueue_s / args.steps * 1e3, 4),
             "pipelined": "batch k's combined check + bisection (second stream) overlap batch k+1's per-vote "
                          "stages; all %d timed batches complete inside the timed region" % args.steps,
         }
