@@ -2054,6 +2054,7 @@ struct ovh_ctx {
   // kernels on the two per-vote streams in turn, so two batches' vote grids co-reside (the
   // spilled vote program's LDS fits seven workgroups per CU); OVH_VOTE_PAIR=0: all on `stream`
   bool vote_pair = VOTE_NSCR > 0;
+  bool gate = true;  // the final streams' residency gate (k_gate); OVH_GATE=0 drops it (A/B)
   uint64_t sm_batches = 0, sm_votes = 0, sm_hashes = 0;
   // ovh_verify_samemsg_device_async: the one-hash plan of sm1_n votes (gid = 0 | head 0 | pairs)
   // and its level offsets; the hash of each slot (32 B per slot)
@@ -2508,10 +2509,10 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
     StageScope p(c, ST_VOTE, st);
     if (key.bytes)
       k_vm_vote<<<nwg, 64, LDS_VOTE, st>>>(n, c->vm_vote, c->vm_fold, c->vm_consts, key.bytes, d_sigs, s, seed, base,
-                                           d_codes, region_F(c, slot, 0), c->vstart, c->vscr[slot]);
+                                           d_codes, region_F(c, slot, 0), c->gate ? c->vstart : nullptr, c->vscr[slot]);
     else
       k_vm_vote_t<<<nwg, 64, LDS_VOTE_T, st>>>(n, c->vm_vote_t, c->vm_fold, c->vm_consts, key.pts, d_sigs, s, seed,
-                                               base, d_codes, region_F(c, slot, 0), c->vstart, c->vscr[slot]);
+                                               base, d_codes, region_F(c, slot, 0), c->gate ? c->vstart : nullptr, c->vscr[slot]);
     c->vlaunched += nwg;
     c->clk_wgs = nwg < VM_CLOCK_WGS ? nwg : VM_CLOCK_WGS;
     c->clk_table = key.bytes == nullptr;
@@ -2657,7 +2658,7 @@ static int side_front(ovh_ctx* c, int slot, uint32_t n, bool pipe, uint32_t unti
   HIPCHK(hipEventRecord(c->ev_front[slot], vst ? vst : c->stream));
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
   const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
-  if (pipe) k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
+  if (pipe && c->gate) k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
   *m = groups_of(n);
   *reg = 1;
   k_vm_fold<VM_FOLD_UNITS><<<(*m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, fst>>>(
@@ -2822,7 +2823,7 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
     CHK(fold_down(c, slot, vst, VM_SLICES, &reg, &m, 4));
     HIPCHK(hipEventRecord(c->ev_front[slot], vst));
     HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
-    if (pipe) {
+    if (pipe && c->gate) {
       const uint32_t nwg = ((uint32_t)n + VM_SLICES - 1) / VM_SLICES;
       k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
     }
@@ -3590,6 +3591,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   if (const char* e = getenv("OVH_FOLD_SIDE")) c->fold_side = atoi(e) != 0;
   if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
   if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e);
+  if (const char* e = getenv("OVH_GATE")) c->gate = atoi(e) != 0;
   if (const char* e = getenv("OVH_VOTE_PAIR")) {
     c->vote_pair = atoi(e) != 0;
     c->npair = atoi(e) >= 3 ? 3 : atoi(e) == 1 ? 1 : 2;
