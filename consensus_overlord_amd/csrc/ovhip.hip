@@ -9,6 +9,9 @@
 //                 the workgroup's 4 votes' f into one partial (level 0; 1 if the vote failed)
 //   k_vm_vote_t   the same with the public key from the device validator table (or a QC's
 //                 aggregated key): no decompression / subgroup check of the key
+//                 (both programs keep <= 90 values in LDS and spill the rest to a per-vote
+//                 scratch through side words, so a CU holds eight vote workgroups: pipelined
+//                 batches put their vote grids on two streams in turn and two co-reside)
 //   k_vm_fold     fold levels: 4 partials -> (prod f, sum S); level 1 = groups of 16 votes
 //   k_msm_*       Pippenger MSM of S = sum r_i sigma_i (msm.hpp), on the final stream
 //   k_vm_final    one wave: prod f * Miller(-G1, S) -> final exponentiation == 1 ?
