@@ -2058,6 +2058,19 @@ struct ovh_ctx {
   // spilled vote program's LDS fits seven workgroups per CU); OVH_VOTE_PAIR=0: all on `stream`
   bool vote_pair = VOTE_NSCR > 0;
   bool gate = true;  // the final streams' residency gate (k_gate); OVH_GATE=0 drops it (A/B)
+  // pair_sync (OVH_PAIR_SYNC=1, A/B): a batch's vote grid waits for the next batch, and the two
+  // grids start together, one per stream of the pair (their inputs are staged per slot at the
+  // call, so the caller may reuse its buffers at once); a lone pending batch is launched by the
+  // next slot taken, any synchronisation or ovh_batch_wait. r04an: 1,276k verifs/s against
+  // 1,280k free-running -- the grids were not losing to a staggered start; off by default
+  bool pair_sync = false;
+  struct {
+    bool on = false;
+    int slot = 0;
+    uint32_t n = 0;
+    int32_t* codes = nullptr;
+  } pend;
+  uint8_t* pstage[OVH_BATCH_SLOTS] = {};  // staged sigs | pks of a pending / paired batch
   uint64_t sm_batches = 0, sm_votes = 0, sm_hashes = 0;
   // ovh_verify_samemsg_device_async: the one-hash plan of sm1_n votes (gid = 0 | head 0 | pairs)
   // and its level offsets; the hash of each slot (32 B per slot)
@@ -2330,7 +2343,10 @@ static Slab region_S(ovh_ctx* c, int slot, int r) {
               c->red_cap};
 }
 
+static int pair_flush(ovh_ctx* c);
+
 static int sync_all(ovh_ctx* c) {
+  CHK(pair_flush(c));  // a batch waiting for its pair partner is launched first
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->fstream));
   HIPCHK(hipStreamSynchronize(c->fstream2));
@@ -2382,9 +2398,10 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
   CHK(sync_all(c));
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
-                    (void*)c->vscr[k]})
+                    (void*)c->vscr[k], (void*)c->pstage[k]})
       if (p) (void)hipFree(p);
     c->state_slot[k] = c->red_slot[k] = c->msm_buf[k] = c->vscr[k] = nullptr;
+    c->pstage[k] = nullptr;
     c->grp_ok[k] = nullptr;
     c->slot_n[k] = 0;
   }
@@ -2397,6 +2414,7 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
     HIPCHK(hipMalloc(&c->grp_ok[k], ((size_t)cap / GROUP_VOTES + 1) * 4));
     HIPCHK(hipMalloc(&c->msm_buf[k], msm_words(cap) * 4));
     if (VOTE_NSCR) HIPCHK(hipMalloc(&c->vscr[k], (size_t)cap * VOTE_NSCR * 12 * 4));
+    if (c->vote_pair) HIPCHK(hipMalloc(&c->pstage[k], (size_t)cap * 144));
   }
   c->cap = cap;
   return 0;
@@ -2436,7 +2454,8 @@ static int ensure_in(ovh_ctx* c, size_t bytes) {
 
 // Batch state slot k for the next batch on the main stream: the stream first waits until the
 // final stream has finished with the slot's previous batch (its bisection reads that state).
-static int take_slot(ovh_ctx* c, int* slot) {
+static int take_slot(ovh_ctx* c, int* slot, bool keep_pending = false) {
+  if (!keep_pending) CHK(pair_flush(c));  // its slot must be in flight before the ring moves on
   const int k = (int)(c->pipe_k % OVH_BATCH_SLOTS);
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_back[k], 0));
   const uint32_t q = c->pipe_k % c->nfin;
@@ -2479,8 +2498,12 @@ struct KeySrc {
 // Per-vote stages of a batch in `slot`: hash_to_field, the vote kernel with fold level 0 fused
 // (-> R0), fold level 1 (-> R1: one partial per 16-vote group). alone: the batch's combined
 // check covers only this batch (not a shard of a larger combined check).
+static int batch_vote(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, KeySrc key, int32_t* d_codes,
+                      bool fold1, hipStream_t st);
+
 static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
-                       int32_t* d_codes, bool fold1 = true, bool alone = false, hipStream_t vst = nullptr) {
+                       int32_t* d_codes, bool fold1 = true, bool alone = false, hipStream_t vst = nullptr,
+                       bool launch_vote = true) {
   Slab s{c->state_slot[slot], c->cap};
   hipStream_t st = vst ? vst : c->stream;
   // with a per-vote stream of the pair: hash_to_field on `stream` (after the caller's work and
@@ -2495,16 +2518,28 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   if (n == 1 && alone) base = UNIT_BASE;
   c->slot_seed[slot] = seed;
   c->slot_base[slot] = base;
-  const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
   {  // hash_to_field on the main stream: its inputs are ready in that stream's order (the
      // staging copies, or a caller's writes on ovh_stream)
     StageScope p(c, ST_H2F, c->stream);
     k_h2f<<<nblk(n), WG, 0, c->stream>>>(n, d_hashes, c->xmd, s);
   }
-  if (st != c->stream) {
+  if (st != c->stream || !launch_vote) {
     HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
-    HIPCHK(hipStreamWaitEvent(st, c->ev_front[slot], 0));
+    if (launch_vote) HIPCHK(hipStreamWaitEvent(st, c->ev_front[slot], 0));
   }
+  c->slot_n[slot] = n;
+  c->last_n = n;
+  if (!launch_vote) return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
+  return batch_vote(c, slot, n, d_sigs, key, d_codes, fold1, st);
+}
+
+// The vote kernel of the batch in `slot` on stream st (its hash_to_field done in st's order),
+// then fold level 1 when fold1.
+static int batch_vote(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, KeySrc key, int32_t* d_codes,
+                      bool fold1, hipStream_t st) {
+  Slab s{c->state_slot[slot], c->cap};
+  const uint64_t seed = c->slot_seed[slot], base = c->slot_base[slot];
+  const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
   const bool vev = (c->flags & OVH_FLAG_PROFILE) != 0;
   const uint32_t vk = c->vev_n % ovh_ctx::VEV_CAP;
   if (vev) HIPCHK(hipEventRecord(c->vev0[vk], st));
@@ -2531,8 +2566,6 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
         nwg, c->vm_fold, c->vm_consts, region_F(c, slot, 0), region_S(c, slot, 0), region_F(c, slot, 1), nullptr);
   }
   HIPCHK(hipGetLastError());
-  c->slot_n[slot] = n;
-  c->last_n = n;
   return 0;
 }
 
@@ -2801,10 +2834,67 @@ static int verify_small_locked(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, co
   return 0;
 }
 
+// The back of a pipelined batch in `slot` whose hash_to_field ran on `stream` (ev_front[slot]):
+// its vote kernel on per-vote stream st (after `also`, when given), then the fold levels, MSM,
+// combined check and device-gated bisection on the slot's final stream.
+static int pair_back(ovh_ctx* c, int slot, uint32_t n, int32_t* d_codes, hipStream_t st, hipEvent_t also) {
+  HIPCHK(hipStreamWaitEvent(st, c->ev_front[slot], 0));
+  if (also) HIPCHK(hipStreamWaitEvent(st, also, 0));
+  const uint8_t* ps = c->pstage[slot];
+  CHK(batch_vote(c, slot, n, ps, KeySrc{ps + (size_t)n * 96, PkSrc{}}, d_codes, false, st));
+  hipStream_t fst = c->fs[slot];
+  uint32_t m;
+  int reg;
+  CHK(side_front(c, slot, n, true, 4, &reg, &m, st));
+  int32_t* verdict = c->result + RES_BATCH + slot;
+  CHK(enqueue_msm(c, fst, slot, n, d_codes));
+  enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict, msm_S(c, slot));
+  enqueue_bisect(c, fst, slot, n, d_codes, verdict);
+  HIPCHK(hipEventRecord(c->ev_back[slot], fst));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+static int pair_flush(ovh_ctx* c) {
+  if (!c->pend.on) return 0;
+  c->pend.on = false;
+  return pair_back(c, c->pend.slot, c->pend.n, c->pend.codes, c->pstream[0], nullptr);
+}
+
+// pair_sync (ovh_verify_batch_device_async on the per-vote pair): stage the batch's signatures
+// and keys in its slot, run its hash_to_field; the first of two batches waits (pend), the second
+// launches both vote grids together -- one per stream of the pair, both after the second's
+// hash_to_field -- so they co-reside from their first workgroup to their last instead of
+// starting staggered behind each other's tails.
+static int verify_pair_locked(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
+                              const uint8_t* d_pks, int32_t* d_codes) {
+  int slot;
+  CHK(take_slot(c, &slot, true));
+  uint8_t* ps = c->pstage[slot];
+  HIPCHK(hipMemcpyAsync(ps, d_sigs, (size_t)n * 96, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(ps + (size_t)n * 96, d_pks, (size_t)n * 48, hipMemcpyDeviceToDevice, c->stream));
+  CHK(batch_front(c, slot, n, ps, d_hashes, KeySrc{ps + (size_t)n * 96, PkSrc{}}, d_codes, false, true, nullptr, false));
+  if (!c->pend.on) {
+    c->pend.on = true;
+    c->pend.slot = slot;
+    c->pend.n = n;
+    c->pend.codes = d_codes;
+    return 0;
+  }
+  const int ps0 = c->pend.slot;
+  const uint32_t n0 = c->pend.n;
+  int32_t* codes0 = c->pend.codes;
+  c->pend.on = false;
+  CHK(pair_back(c, ps0, n0, codes0, c->pstream[0], c->ev_front[slot]));
+  return pair_back(c, slot, n, d_codes, c->pstream[1], nullptr);
+}
+
 static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
                                int32_t* d_codes, bool pipe = false) {
   CHK(ensure_cap(c, n));
   if (n >= 2 && n <= c->small_max) return verify_small_locked(c, (uint32_t)n, d_sigs, d_hashes, key, d_codes);
+  if (pipe && c->vote_pair && c->pair_sync && c->fold_side && key.bytes && c->pstage[0] && c->npair == 2)
+    return verify_pair_locked(c, (uint32_t)n, d_sigs, d_hashes, key.bytes, d_codes);
   int slot;
   CHK(take_slot(c, &slot));
   const bool side = c->fold_side;
@@ -3595,6 +3685,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
   if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e);
   if (const char* e = getenv("OVH_GATE")) c->gate = atoi(e) != 0;
+  if (const char* e = getenv("OVH_PAIR_SYNC")) c->pair_sync = atoi(e) != 0;
   if (const char* e = getenv("OVH_VOTE_PAIR")) {
     c->vote_pair = atoi(e) != 0;
     c->npair = atoi(e) >= 3 ? 3 : atoi(e) == 1 ? 1 : 2;
@@ -3747,7 +3838,7 @@ static void destroy_one(ovh_ctx* c) {
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
-                    (void*)c->gslab[k], (void*)c->vscr[k]})
+                    (void*)c->gslab[k], (void*)c->vscr[k], (void*)c->pstage[k]})
       if (p) (void)hipFree(p);
   for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vstart, (void*)c->vm_consts,
                   (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
