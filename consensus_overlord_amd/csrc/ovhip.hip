@@ -337,68 +337,326 @@ __device__ __forceinline__ void vote_stagger() {
 #endif
 }
 
-// Per vote: VM "vote" program + reference-precedence code + the vote's f contribution (its
-// sigma / tau planes feed the MSM). LDS: constants, then VM_SLICES x (VM_VOTE_NSLOTS slots).
-__global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
-                                                const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs,
-                                                Slab s, uint64_t seed, uint64_t base, int32_t* __restrict__ codes,
-                                                Slab part0, unsigned long long* vstart, uint32_t* __restrict__ scr) {
-  __builtin_amdgcn_s_setprio(2);  // per-vote stages outrank a co-resident final-stream wave
-  if (vstart && threadIdx.x == 0) atomicAdd(vstart, 1ull);  // resident (k_gate)
-  extern __shared__ uint4 lds4[];
-  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+// Public keys given as points (ovh_set_validators table, or a QC's aggregated key): planes
+// X, Y, Z (homogeneous projective, Montgomery) of `cap` entries, plus per-entry flags.
+#define PKF_PARSE 1u  // the 48 bytes did not parse -> "lose public key" (102)
+#define PKF_INF 2u    // the point at infinity      -> BLST_PK_IS_INFINITY (6) at verify
+#define PKF_GRP 4u    // not in G1                  -> BLST_POINT_NOT_IN_GROUP (3) at verify
+struct PkSrc {
+  const uint32_t* planes;
+  uint32_t cap;
+  const uint32_t* flags;
+  const int32_t* idx;  // vote i uses entry idx[i] (null: entry i)
+};
+
+// ------------------------------------------------------------------------ the vote pool
+// The per-vote work of every batch ("Vote pool"). A batch is published to a
+// device queue as a descriptor; the pool kernel's workgroups (one wave each, four 16-lane vote
+// slices) claim 4-vote quads from the queue in publication order -- across batches -- and run
+// the "vote" / "vote_t" program on each, so a workgroup that finishes batch k's quad takes batch
+// k + 1's at once: no grid boundary, no per-grid tail, no stream-order wait between batches. One
+// pool grid is launched (on the pool stream) after each publication, which guarantees that some
+// grid runs after the batch appeared; a workgroup exits when the queue is empty, so the grid
+// launched for batch k + 1 usually finds batch k's grid still working and its own workgroups do
+// nothing. A batch's final stream waits for its quads with k_pool_wait (done counter).
+//
+// Queue words (uint64, each on its own 128-byte line): cur = the oldest batch that may still have
+// unclaimed quads; npub = batches published; slot_of[seq % POOL_SEQR] = the batch slot of batch
+// seq; per slot, claim = (seq << 32) | quads claimed of the slot's batch and done = quads
+// completed. A workgroup claims with ONE fetch-add on the claim word of batch cur's slot (no
+// compare-and-swap window: r05a's CAS on a shared cursor handed out one quad per ~25 us). The
+// claim word carries the batch it counts for, so a claim through a stale cur / slot_of is still
+// exact: it is quad `count` of batch `seq` (processed iff count < that batch's nq, after its
+// publication). Batches take batch slots (take_slot) and a slot is reused only after its batch
+// completed; every quad a workgroup claimed below nq is processed, so a slot is never
+// republished under a workgroup that holds one of its quads.
+#define POOL_SEQR 16u
+#define POOL_QW 16u  // uint64 words per 128-byte line
+enum : uint32_t {
+  PQ_CUR = 0,
+  PQ_NPUB = POOL_QW,
+  PQ_SLOTOF = 2 * POOL_QW,
+  PQ_NANN = 3 * POOL_QW,
+  PQ_DONE = 4 * POOL_QW,
+  PQ_CLAIM = PQ_DONE + OVH_BATCH_SLOTS * POOL_QW,
+};
+constexpr uint32_t PQ_WORDS = PQ_CLAIM + OVH_BATCH_SLOTS * POOL_QW;
+static_assert(POOL_SEQR > OVH_BATCH_SLOTS && POOL_SEQR / 2 <= POOL_QW, "pool queue layout");
+// A workgroup that finds the queue empty polls it for POOL_IDLE_TICKS (20 us) before it exits --
+// or, while a batch is announced but not yet published (nann > npub: its staging and
+// hash_to_field are on ovh_stream), for up to POOL_WAIT_TICKS (20 ms). r05h: without the
+// announcement the first grid's spare workgroups left during the next batch's hash_to_field and
+// the pool ran the rest of the run on the 1,024 workgroups that had found a quad.
+#define POOL_IDLE_TICKS 2000ull
+#define POOL_WAIT_TICKS 2000000ull
+
+struct PoolBatch {  // one published batch (written by k_pool_publish, read by the pool)
+  uint64_t seq;          // its sequence number (written last: a claimer checks it, pool_claim)
+  uint32_t n, nq;
+  uint32_t table;        // 1: keys are points (program vote_t), 0: n x 48 compressed bytes (vote)
+  uint32_t has_idx;      // vote_t: vote i uses table entry idx[i] (staged after the keys), else i
+  uint64_t seed, base;   // RLC coefficients (vote_scalar)
+  int32_t* codes;
+  const uint32_t* planes;  // vote_t: key points (X, Y, Z planes of `pcap` entries) and flags
+  const uint32_t* flags;
+  uint32_t pcap, cap;    // cap: the state slab's
+  uint32_t* state;       // the slot's state slab (u planes in; sigma, tau, f planes out)
+  uint32_t* part0;       // fold region R0 (one partial per quad) of `part_cap` entries
+  const uint8_t* stage;  // staged signatures | keys | table indices (k_pool_stage)
+  uint64_t* clk;         // OVH_FLAG_VM_CLOCK: per-workgroup stamps, else null
+  uint32_t part_cap, pad;
+};
+
+// The pool kernel's arguments: the queue, the descriptors, the two vote programs' instruction
+// and side-word streams, the fold program, the constant table and the spill scratch. Everything
+// per batch is in the descriptor and read where it is used.
+struct PoolArgs {
+  uint64_t* q;
+  const PoolBatch* descs;
+  const uint4* pv_code;
+  const uint32_t* pv_side;
+  const uint4* pt_code;
+  const uint32_t* pt_side;
+  const uint4* fold_code;
+  const uint32_t* cst;
+  uint32_t* scr;  // VM_SLICES x VOTE_NSCR entries per workgroup
+};
+
+__device__ __forceinline__ uint64_t* pq_done(uint64_t* q, uint32_t slot) { return q + PQ_DONE + slot * POOL_QW; }
+__device__ __forceinline__ uint64_t* pq_claim(uint64_t* q, uint32_t slot) { return q + PQ_CLAIM + slot * POOL_QW; }
+__device__ __forceinline__ uint32_t* pq_slot_of(uint64_t* q) { return reinterpret_cast<uint32_t*>(q + PQ_SLOTOF); }
+__device__ __forceinline__ uint64_t qld(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Publish batch `seq` in slot `slot` (one lane; ovh_stream, after the batch's hash_to_field and
+// staging): the descriptor, then (behind a release) its seq, done = 0, the claim word and
+// slot_of, then (behind a release) npub.
+__global__ __launch_bounds__(64) void k_pool_publish(PoolBatch b, uint32_t slot, uint64_t seq, uint64_t* q,
+                                                     PoolBatch* descs) {
+  if (threadIdx.x) return;
+  b.seq = ~0ull;
+  descs[slot] = b;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(&descs[slot].seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(pq_done(q, slot), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(pq_claim(q, slot), seq << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(pq_slot_of(q) + seq % POOL_SEQR, slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (MI355X_MICROARCH.md: the wait the compiler may drop)
+  __hip_atomic_store(q + PQ_NPUB, seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Announce batch seq: nann = seq + 1 tells idle pool workgroups that a publication is on its way
+// (the announcement stream's write, when the host enqueues the batch; this kernel only if the
+// stream write is not available).
+__global__ __launch_bounds__(64) void k_pool_announce(uint64_t* q, uint64_t n) {
+  if (threadIdx.x == 0) __hip_atomic_store(q + PQ_NANN, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Claim the next quad (the whole wave, in wave-uniform control flow: every lane reads the same
+// queue words, lane 0 alone performs the atomics and the result is broadcast -- r05c ran the
+// claim loop in a lane-0 branch, and the workgroup's later quads ran with lane 0 alone active).
+// Returns 1 and the quad's slot and index, or 0 when the queue stays empty for
+// POOL_IDLE_TICKS. Every quad is handed out by exactly one fetch-add on its batch's claim word; a
+// claim past the batch's nq moves `cur` on.
+__device__ __forceinline__ uint64_t lane0_fetch_add(uint64_t* p, uint64_t v) {
+  uint64_t r = 0;
+  if (threadIdx.x == 0) r = __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32) |
+         __builtin_amdgcn_readfirstlane((uint32_t)r);
+}
+__device__ __forceinline__ void lane0_cas(uint64_t* p, uint64_t expect, uint64_t want) {
+  if (threadIdx.x == 0) {
+    uint64_t e = expect;
+    (void)__hip_atomic_compare_exchange_strong(p, &e, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__device__ __forceinline__ uint64_t wclock() {
+  const uint64_t t = wall_clock64();
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(t >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)t);
+}
+__device__ __forceinline__ uint64_t qldu(const uint64_t* p) {
+  const uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+__device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* slot_out, uint32_t* quad_out) {
+  uint64_t t0 = wclock();
+#pragma unroll 1
+  for (uint32_t tries = 0; tries < (1u << 22); ++tries) {
+    const uint64_t s = qldu(q + PQ_CUR), np = qldu(q + PQ_NPUB);
+    if (s >= np) {
+      const uint64_t idle = wclock() - t0;
+      if (idle > POOL_WAIT_TICKS || (idle > POOL_IDLE_TICKS && qldu(q + PQ_NANN) <= np)) return 0;
+      __builtin_amdgcn_s_sleep(8);
+      continue;
+    }
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(pq_slot_of(q) + s % POOL_SEQR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint64_t old = lane0_fetch_add(pq_claim(q, slot), 1ull);
+    const uint64_t seq = old >> 32;
+    const uint32_t idx = (uint32_t)old;
+    // the claim counts for batch `seq` (a stale slot_of may have led here): wait for its publication
+    const uint64_t tw = wclock();
+    while (qldu(q + PQ_NPUB) <= seq && wclock() - tw < 100000000ull) __builtin_amdgcn_s_sleep(2);
+    const uint32_t nq = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&descs[slot].nq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint64_t dseq = qldu(&descs[slot].seq);
+    // dseq != seq: the slot was republished, so batch seq completed -- every quad of it below nq
+    // was claimed by others, this one is past its end
+    const bool mine = dseq == seq && idx < nq;
+    // batch s is fully claimed when this claim went past its end, or when its slot already holds
+    // a later batch (seq != s: a slot is republished only after its batch completed): move cur on
+    // (whoever wins; a claim that took exactly the last quad does not, the next claimer does)
+    if (seq != s || !mine) lane0_cas(q + PQ_CUR, s, s + 1);
+    if (mine) {
+      *slot_out = slot;
+      *quad_out = idx;
+      return 1;
+    }
+    t0 = wclock();  // progress: the idle window restarts
+  }
+  return 0;
+}
+
+// Descriptor fields are read where they are used (relaxed agent-scope loads: vector loads, never
+// the scalar cache), so no batch state stays live across the VM program: the vote program
+// already needs every VGPR of a two-waves-per-SIMD budget and most SGPRs.
+template <typename T>
+__device__ __forceinline__ T dget(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T* dgetp(T* const* p) {
+  return reinterpret_cast<T*>(__hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+template <typename T>
+__device__ __forceinline__ T* unip(T* p) {
+  return reinterpret_cast<T*>(uni64(reinterpret_cast<uint64_t>(p)));
+}
+
+// One quad of a batch: votes 4 quad .. 4 quad + 3 on the four slices -- inputs, the vote / vote_t
+// program, the per-vote code in the reference's precedence, then fold level 0 of the quad's f
+// (fused: -> partial `quad` of R0, the identity for failed votes). Only the VM's own operands
+// stay in registers across the program: the slot and quad wait in the LDS header words of slice
+// 2 and the clock stamps (OVH_FLAG_VM_CLOCK) in those of slices 0 and 1.
+template <bool TABLE>
+__device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, uint32_t quad_in, uint32_t* lds) {
+  constexpr uint32_t NSLOTS = TABLE ? VM_VOTE_T_NSLOTS : VM_VOTE_NSLOTS;
+  constexpr uint32_t STRIDE = TABLE ? VOTE_T_STRIDE_W : VOTE_STRIDE_W;
+  constexpr uint32_t NPH = TABLE ? VM_VOTE_T_NPHASES : VM_VOTE_NPHASES;
+  const uint16_t* IN = TABLE ? VM_VOTE_T_IN : VM_VOTE_IN;
+  const uint16_t* OUT = TABLE ? VM_VOTE_T_OUT : VM_VOTE_OUT;
   uint32_t* cst = lds;
   const uint32_t slice = threadIdx.x / VM_VOTE_W, lane = threadIdx.x % VM_VOTE_W;
-  uint32_t* slots = lds + SLOT_BASE_W + slice * VOTE_STRIDE_W;
-  uint32_t* hdr = slots + VM_VOTE_NSLOTS * 12;  // [pflags, code]
-  const uint32_t i = blockIdx.x * VM_SLICES + slice;
-  const bool active = i < n;
-  load_consts(cst, cst_g, VM_NCONST);
-  if (active) {
-    if (lane == 0) {
-      uint32_t x[12], bad, inf, sort, xz;
-      parse_hdr(pks + (size_t)i * 48, 48, x, x, bad, inf, sort, xz);
-      slot_put(slots, VM_VOTE_IN[VM_VOTE_IN_PK_X], x);
-      slot_flag(slots, VM_VOTE_IN[VM_VOTE_IN_PK_SORT], sort);
-      hdr[0] = bad | inf << 1 | xz << 2;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * STRIDE;
+  uint32_t* hdr = slots + NSLOTS * 12;  // [sig flags, pk flags, (slice 0..2: stamps, slot, quad)]
+  uint32_t* park = lds + SLOT_BASE_W + 2 * STRIDE + NSLOTS * 12 + 2;  // slice 2's hdr[2..3]
+  {
+    const PoolBatch* bd = a.descs + slot_in;
+    const uint32_t i = quad_in * VM_SLICES + slice;
+    const uint32_t n = uni(dget(&bd->n));
+    const bool active = i < n;
+    const uint8_t* sigs = unip(dgetp(&bd->stage));
+    const Slab s{unip(dgetp(&bd->state)), uni(dget(&bd->cap))};
+    if (active) {
+      if (lane == 0) {
+        uint32_t x1[12], x0[12], bad, inf, sort, xz;
+        parse_hdr(sigs + (size_t)i * 96, 96, x1, x0, bad, inf, sort, xz);
+        slot_put(slots, IN[TABLE ? VM_VOTE_T_IN_SIG_X1 : VM_VOTE_IN_SIG_X1], x1);
+        slot_put(slots, IN[TABLE ? VM_VOTE_T_IN_SIG_X0 : VM_VOTE_IN_SIG_X0], x0);
+        slot_flag(slots, IN[TABLE ? VM_VOTE_T_IN_SIG_SORT : VM_VOTE_IN_SIG_SORT], sort);
+        hdr[0] = bad | inf << 1 | xz << 2;
+      } else if (lane >= 2 && lane < 6) {
+        Fp u;
+        s.ld(u, S_U + (lane - 2), i);
+        slot_put(slots, IN[(TABLE ? VM_VOTE_T_IN_U00 : VM_VOTE_IN_U00) + (lane - 2)], u.v);
+      }
     }
-  }
-  __syncthreads();
-  if (active) {
-    if (lane == 1) {
-      uint32_t x1[12], x0[12], bad, inf, sort, xz;
-      parse_hdr(sigs + (size_t)i * 96, 96, x1, x0, bad, inf, sort, xz);
-      slot_put(slots, VM_VOTE_IN[VM_VOTE_IN_SIG_X1], x1);
-      slot_put(slots, VM_VOTE_IN[VM_VOTE_IN_SIG_X0], x0);
-      slot_flag(slots, VM_VOTE_IN[VM_VOTE_IN_SIG_SORT], sort);
-      hdr[0] |= (bad | inf << 1 | xz << 2) << 8;
-    } else if (lane >= 2 && lane < 6) {
-      Fp u;
-      s.ld(u, S_U + (lane - 2), i);
-      slot_put(slots, VM_VOTE_IN[VM_VOTE_IN_U00 + (lane - 2)], u.v);
+    if (threadIdx.x == 0) {
+      park[0] = slot_in;
+      park[1] = quad_in;
     }
+    __syncthreads();
+    if (active) {
+      if constexpr (TABLE) {
+        const int32_t* idx = reinterpret_cast<const int32_t*>(sigs + (size_t)n * 144);
+        const uint32_t e = uni(dget(&bd->has_idx)) ? (uint32_t)idx[i] : i;
+        if (lane == 1) {
+          hdr[1] = unip(dgetp(&bd->flags))[e];
+        } else if (lane >= 6 && lane < 9) {
+          Fp v;
+          Slab{const_cast<uint32_t*>(unip(dgetp(&bd->planes))), uni(dget(&bd->pcap))}.ld(v, lane - 6, e);
+          slot_put(slots, IN[VM_VOTE_T_IN_PK_X + (lane - 6)], v.v);
+        }
+      } else {
+        if (lane == 1) {
+          uint32_t x[12], bad, inf, sort, xz;
+          parse_hdr(sigs + (size_t)n * 96 + (size_t)i * 48, 48, x, x, bad, inf, sort, xz);
+          slot_put(slots, IN[VM_VOTE_IN_PK_X], x);
+          slot_flag(slots, IN[VM_VOTE_IN_PK_SORT], sort);
+          hdr[1] = bad | inf << 1 | xz << 2;
+        }
+      }
+    }
+    if (threadIdx.x == 0 && dgetp(&bd->clk)) {
+      const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t* h0 = lds + SLOT_BASE_W + NSLOTS * 12 + 2;
+      uint32_t* h1 = lds + SLOT_BASE_W + STRIDE + NSLOTS * 12 + 2;
+      h0[0] = (uint32_t)t0;
+      h0[1] = (uint32_t)(t0 >> 32);
+      h1[0] = (uint32_t)r0;
+      h1[1] = (uint32_t)(r0 >> 32);
+    }
+    __syncthreads();
+    const uint64_t scalar = vote_scalar(uni64(dget(&bd->seed)), uni64(dget(&bd->base)), i);
+    vm::run<true>(TABLE ? a.pt_code : a.pv_code, NPH, VM_VOTE_W, lane, active, slots, cst, scalar,
+                  vm::Out{s.p, s.cap, i}, nullptr, TABLE ? a.pt_side : a.pv_side,
+                  a.scr + (size_t)blockIdx.x * VM_SLICES * VOTE_NSCR * 12 + slice * VOTE_NSCR * 12);
   }
-  __syncthreads();
-  vote_stagger();
-  ClockStamp cs;
-  cs.begin(prog.clk);
-  vm::run<(VM_VOTE_NSCR > 0)>(prog.code, VM_VOTE_NPHASES, VM_VOTE_W, lane, active, slots, cst,
-                              vote_scalar(seed, base, i), vm::Out{s.p, s.cap, i},
-                              blockIdx.x == 0 ? prog.trace : nullptr, prog.side, scr + (size_t)i * VOTE_NSCR * 12);
-  cs.end(prog.clk);
-  if (active && lane == 0) {
-    const uint32_t pf = hdr[0];
-    const uint32_t pk_bad = pf & 1, pk_inf = (pf >> 1) & 1, pk_xz = (pf >> 2) & 1;
-    const uint32_t sg_bad = (pf >> 8) & 1, sg_inf = (pf >> 9) & 1, sg_xz = (pf >> 10) & 1;
-    const uint32_t pk_ok = slot_flag_get(slots, VM_VOTE_OUT[VM_VOTE_OUT_PK_OK]);
-    const uint32_t pk_grp = slot_flag_get(slots, VM_VOTE_OUT[VM_VOTE_OUT_PK_GRP]);
-    const uint32_t sg_ok = slot_flag_get(slots, VM_VOTE_OUT[VM_VOTE_OUT_SIG_OK]);
-    const uint32_t sg_grp = slot_flag_get(slots, VM_VOTE_OUT[VM_VOTE_OUT_SIG_GRP]);
-    const uint32_t h_inf = slot_flag_get(slots, VM_VOTE_OUT[VM_VOTE_OUT_H_INF]);
+  // after the program: the slot and quad back from LDS (run ends with an LDS wait + barrier)
+  const uint32_t slot = uni(park[0]), quad = uni(park[1]);
+  const PoolBatch* bd = a.descs + slot;
+  const uint32_t i = quad * VM_SLICES + slice;
+  const uint32_t n = uni(dget(&bd->n));
+  int32_t* codes = unip(dgetp(&bd->codes));
+  if (uint64_t* clk = dgetp(&bd->clk); clk && threadIdx.x == 0 && blockIdx.x < VM_CLOCK_WGS) {
+    const uint32_t* h0 = lds + SLOT_BASE_W + NSLOTS * 12 + 2;
+    const uint32_t* h1 = lds + SLOT_BASE_W + STRIDE + NSLOTS * 12 + 2;
+    const uint64_t t0 = h0[0] | (uint64_t)h0[1] << 32, r0 = h1[0] | (uint64_t)h1[1] << 32;
+    clk[2 * blockIdx.x] = __builtin_amdgcn_s_memtime() - t0;
+    clk[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() - r0;
+  }
+  if (i < n && lane == 0) {
+    const uint32_t sf = hdr[0], pf = hdr[1];
+    const uint32_t sg_bad = sf & 1, sg_inf = (sf >> 1) & 1, sg_xz = (sf >> 2) & 1;
+    const uint32_t sg_ok = slot_flag_get(slots, OUT[TABLE ? VM_VOTE_T_OUT_SIG_OK : VM_VOTE_OUT_SIG_OK]);
+    const uint32_t sg_grp = slot_flag_get(slots, OUT[TABLE ? VM_VOTE_T_OUT_SIG_GRP : VM_VOTE_OUT_SIG_GRP]);
+    const uint32_t h_inf = slot_flag_get(slots, OUT[TABLE ? VM_VOTE_T_OUT_H_INF : VM_VOTE_OUT_H_INF]);
     // consensus.rs:397-416: pk parse (102) > sig parse (1..3) > [core_verify] sig group (3) >
     // pk infinity (6) > pk group (3) > H(m) = O or sig = O (5) > pairing (batch)
+    uint32_t pk_parse, pk_inf, pk_grp;
+    if constexpr (TABLE) {
+      pk_parse = pf & PKF_PARSE;
+      pk_inf = pf & PKF_INF;
+      pk_grp = !(pf & PKF_GRP);
+    } else {
+      const uint32_t pk_bad = pf & 1, pk_xz = (pf >> 2) & 1;
+      pk_inf = (pf >> 1) & 1;
+      const uint32_t pk_ok = slot_flag_get(slots, OUT[VM_VOTE_OUT_PK_OK]);
+      pk_grp = slot_flag_get(slots, OUT[VM_VOTE_OUT_PK_GRP]);
+      pk_parse = pk_bad || (!pk_inf && (!pk_ok || pk_xz));
+    }
     int32_t c;
-    if (pk_bad || (!pk_inf && (!pk_ok || pk_xz))) c = OVH_ERR_PUBKEY;
+    if (pk_parse) c = OVH_ERR_PUBKEY;
     else if (sg_bad) c = BLST_BAD_ENCODING;
     else if (!sg_inf && !sg_ok) c = BLST_POINT_NOT_ON_CURVE;
     else if (!sg_inf && (sg_xz || !sg_grp)) c = BLST_POINT_NOT_IN_GROUP;
@@ -408,14 +666,75 @@ __global__ __launch_bounds__(64) void k_vm_vote(uint32_t n, VmDev prog, VmDev fo
     else c = 0;
     codes[i] = c;
   }
-  // fold level 0, fused: this workgroup's 4 votes -> partial blockIdx.x of part0 (F planes
-  // 0..11, S planes 12..17), the identity for failed votes. The slices' `st` outputs (HBM)
-  // and codes are made visible to the workgroup first; the fold reuses the vote slots' LDS.
+  // fold level 0, fused: the quad's 4 votes -> partial `quad` of R0 (F planes 0..11, S planes
+  // 12..17), the identity for failed votes. The slices' `st` outputs (HBM) and codes are made
+  // visible to the workgroup first; the fold reuses the vote slots' LDS.
   __threadfence();
   __syncthreads();
-  fold_unit(blockIdx.x, n, fold, cst, lds + SLOT_BASE_W, threadIdx.x % VM_FOLD_W,
-            threadIdx.x < VM_FOLD_W && 4 * blockIdx.x < n,
-            Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{nullptr, 0}, part0, codes);
+  const Slab s{unip(dgetp(&bd->state)), uni(dget(&bd->cap))};
+  VmDev fold{};
+  fold.code = a.fold_code;
+  fold_unit(quad, n, fold, cst, lds + SLOT_BASE_W, threadIdx.x % VM_FOLD_W, threadIdx.x < VM_FOLD_W,
+            Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{nullptr, 0},
+            Slab{unip(dgetp(&bd->part0)), uni(dget(&bd->part_cap))}, codes);
+  // the quad's codes, planes and partial, then its done count (k_pool_wait)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(pq_done(a.q, slot), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The pool: each workgroup claims quads until the queue stays empty (pool_claim), then exits.
+// LDS: constants + four slices of the larger of the vote / vote_t slot files; scratch: the
+// workgroup's own spill area (4 x VOTE_NSCR entries), reused quad after quad. Two waves per SIMD
+// are declared (the register budget that makes two pool workgroups share a SIMD).
+__global__ __launch_bounds__(64, 2) void k_vm_pool(PoolArgs a) {
+  __builtin_amdgcn_s_setprio(2);  // per-vote work outranks a co-resident final-stream wave
+  extern __shared__ uint4 lds4[];
+  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
+  load_consts(lds, a.cst, VM_NCONST);
+  vote_stagger();
+#pragma unroll 1
+  for (;;) {
+    uint32_t slot = 0, quad = 0;
+    if (!pool_claim(a.q, a.descs, &slot, &quad)) break;
+    slot = uni(slot);
+    quad = uni(quad);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this batch's descriptor and inputs, fresh
+    if (uni(dget(&a.descs[slot].table))) vote_quad<true>(a, slot, quad, lds);
+    else vote_quad<false>(a, slot, quad, lds);
+  }
+}
+
+// A batch's final stream waits here until the pool completed all `nq` quads of the slot's batch
+// (one lane, bounded: after `ticks` of the 100 MHz clock it flags *err and returns, and the host
+// reports OVH_ERR_DEVICE at the next synchronisation).
+__global__ __launch_bounds__(64) void k_pool_wait(uint64_t* q, uint32_t slot, uint32_t nq, uint64_t ticks,
+                                                  uint32_t* err) {
+  if (threadIdx.x) return;
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(pq_done(q, slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nq) {
+    if (wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(32);
+  }
+}
+
+// Staging of a pool batch (ovh_stream, before its publication): the signatures and keys (or
+// table indices) into the slot's own buffer, so the caller's buffers are free once ovh_stream
+// has passed this kernel (the pool reads the batch later, on its own schedule).
+__global__ __launch_bounds__(WG) void k_pool_stage(uint32_t n, const uint8_t* __restrict__ sigs,
+                                                   const uint8_t* __restrict__ pks, const int32_t* __restrict__ idx,
+                                                   uint8_t* __restrict__ dst) {
+  const size_t nb = (size_t)n * 96 + (pks ? (size_t)n * 48 : 0);
+  uint8_t* di = dst + (size_t)n * 144;
+  for (size_t k = (size_t)blockIdx.x * WG + threadIdx.x; k < nb + (idx ? (size_t)n * 4 : 0);
+       k += (size_t)gridDim.x * WG) {
+    if (k < (size_t)n * 96) dst[k] = sigs[k];
+    else if (k < nb) dst[k] = pks[k - (size_t)n * 96];
+    else di[k - nb] = reinterpret_cast<const uint8_t*>(idx)[k - nb];
+  }
 }
 
 // Fold level: SLICES units per 64-thread workgroup (4 on the main stream; 1 on the final
@@ -472,87 +791,6 @@ __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const u
   vm::run(prog.code, VM_FINAL_NPHASES, VM_FINAL_W, lane, true, slots, cst, 0, vm::Out{nullptr, 0, 0},
           blockIdx.x == 0 ? prog.trace : nullptr);
   if (lane == 0) *result = slot_flag_get(slots, VM_FINAL_OUT[0]) ? 1 : 0;
-}
-
-// Public keys given as points (ovh_set_validators table, or a QC's aggregated key): planes
-// X, Y, Z (homogeneous projective, Montgomery) of `cap` entries, plus per-entry flags.
-#define PKF_PARSE 1u  // the 48 bytes did not parse -> "lose public key" (102)
-#define PKF_INF 2u    // the point at infinity      -> BLST_PK_IS_INFINITY (6) at verify
-#define PKF_GRP 4u    // not in G1                  -> BLST_POINT_NOT_IN_GROUP (3) at verify
-struct PkSrc {
-  const uint32_t* planes;
-  uint32_t cap;
-  const uint32_t* flags;
-  const int32_t* idx;  // vote i uses entry idx[i] (null: entry i)
-};
-
-// vote_t: the vote program without the key's decompression / subgroup check. Same outputs
-// (code, stored f and r sigma, fused level-0 fold) as k_vm_vote.
-__global__ __launch_bounds__(64) void k_vm_vote_t(uint32_t n, VmDev prog, VmDev fold, const uint32_t* __restrict__ cst_g,
-                                                  PkSrc pk, const uint8_t* __restrict__ sigs, Slab s, uint64_t seed,
-                                                  uint64_t base, int32_t* __restrict__ codes, Slab part0,
-                                                  unsigned long long* vstart, uint32_t* __restrict__ scr) {
-  __builtin_amdgcn_s_setprio(2);
-  if (vstart && threadIdx.x == 0) atomicAdd(vstart, 1ull);
-  extern __shared__ uint4 lds4[];
-  uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
-  uint32_t* cst = lds;
-  const uint32_t slice = threadIdx.x / VM_VOTE_T_W, lane = threadIdx.x % VM_VOTE_T_W;
-  uint32_t* slots = lds + SLOT_BASE_W + slice * VOTE_T_STRIDE_W;
-  uint32_t* hdr = slots + VM_VOTE_T_NSLOTS * 12;  // [sig flags, pk flags]
-  const uint32_t i = blockIdx.x * VM_SLICES + slice;
-  const bool active = i < n;
-  load_consts(cst, cst_g, VM_NCONST);
-  if (active) {
-    const uint32_t e = pk.idx ? (uint32_t)pk.idx[i] : i;
-    if (lane == 0) {
-      uint32_t x1[12], x0[12], bad, inf, sort, xz;
-      parse_hdr(sigs + (size_t)i * 96, 96, x1, x0, bad, inf, sort, xz);
-      slot_put(slots, VM_VOTE_T_IN[VM_VOTE_T_IN_SIG_X1], x1);
-      slot_put(slots, VM_VOTE_T_IN[VM_VOTE_T_IN_SIG_X0], x0);
-      slot_flag(slots, VM_VOTE_T_IN[VM_VOTE_T_IN_SIG_SORT], sort);
-      hdr[0] = bad | inf << 1 | xz << 2;
-      hdr[1] = pk.flags[e];
-    } else if (lane >= 2 && lane < 6) {
-      Fp u;
-      s.ld(u, S_U + (lane - 2), i);
-      slot_put(slots, VM_VOTE_T_IN[VM_VOTE_T_IN_U00 + (lane - 2)], u.v);
-    } else if (lane >= 6 && lane < 9) {
-      Fp v;
-      Slab{const_cast<uint32_t*>(pk.planes), pk.cap}.ld(v, lane - 6, e);
-      slot_put(slots, VM_VOTE_T_IN[VM_VOTE_T_IN_PK_X + (lane - 6)], v.v);
-    }
-  }
-  __syncthreads();
-  vote_stagger();
-  ClockStamp cs;
-  cs.begin(prog.clk);
-  vm::run<(VM_VOTE_T_NSCR > 0)>(prog.code, VM_VOTE_T_NPHASES, VM_VOTE_T_W, lane, active, slots, cst,
-                                vote_scalar(seed, base, i), vm::Out{s.p, s.cap, i},
-                                blockIdx.x == 0 ? prog.trace : nullptr, prog.side, scr + (size_t)i * VOTE_NSCR * 12);
-  cs.end(prog.clk);
-  if (active && lane == 0) {
-    const uint32_t sf = hdr[0], pf = hdr[1];
-    const uint32_t sg_bad = sf & 1, sg_inf = (sf >> 1) & 1, sg_xz = (sf >> 2) & 1;
-    const uint32_t sg_ok = slot_flag_get(slots, VM_VOTE_T_OUT[VM_VOTE_T_OUT_SIG_OK]);
-    const uint32_t sg_grp = slot_flag_get(slots, VM_VOTE_T_OUT[VM_VOTE_T_OUT_SIG_GRP]);
-    const uint32_t h_inf = slot_flag_get(slots, VM_VOTE_T_OUT[VM_VOTE_T_OUT_H_INF]);
-    int32_t c;  // precedence as k_vm_vote (consensus.rs:397-416)
-    if (pf & PKF_PARSE) c = OVH_ERR_PUBKEY;
-    else if (sg_bad) c = BLST_BAD_ENCODING;
-    else if (!sg_inf && !sg_ok) c = BLST_POINT_NOT_ON_CURVE;
-    else if (!sg_inf && (sg_xz || !sg_grp)) c = BLST_POINT_NOT_IN_GROUP;
-    else if (pf & PKF_INF) c = BLST_PK_IS_INFINITY;
-    else if (pf & PKF_GRP) c = BLST_POINT_NOT_IN_GROUP;
-    else if (h_inf || sg_inf) c = BLST_VERIFY_FAIL;
-    else c = 0;
-    codes[i] = c;
-  }
-  __threadfence();
-  __syncthreads();
-  fold_unit(blockIdx.x, n, fold, cst, lds + SLOT_BASE_W, threadIdx.x % VM_FOLD_W,
-            threadIdx.x < VM_FOLD_W && 4 * blockIdx.x < n,
-            Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{nullptr, 0}, part0, codes);
 }
 
 // One standalone vote (ovh_verify, verify_aggregated_signature: a batch of one needs no RLC
@@ -1514,19 +1752,6 @@ __global__ __launch_bounds__(64) void k_vm_signg(uint32_t n, VmDev p0, VmDev p1,
 
 #include "msm.hpp"
 
-#define GATE_TICKS 30000ull  // 300 us of the 100 MHz wall clock
-// Pipelined batches: holds a final stream until the next vote kernel's workgroups are resident
-// (the vote kernels count their started workgroups into *vstart; target = that count once the
-// next kernel's are placed), so no final-stream workgroup takes the LDS a vote workgroup needs
-// (a vote workgroup that finds none waits for a whole vote duration); gives up after `ticks` of
-// the 100 MHz wall clock (no next batch in flight).
-__global__ __launch_bounds__(64) void k_gate(const unsigned long long* vstart, unsigned long long target, uint64_t ticks) {
-  if (threadIdx.x) return;
-  const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(vstart, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && wall_clock64() - t0 < ticks)
-    __builtin_amdgcn_s_sleep(16);
-}
-
 // Validator table (ovh_set_validators) and the keys of verify_aggregated_signature: one 48-byte
 // compressed key per 16-lane slice (program "pkchk": decompression + G1 subgroup check) -> flags
 // + the point (X : Y : Z) Montgomery, (0 : 1 : 0) for infinity or a failed parse. Flag precedence
@@ -1963,37 +2188,43 @@ struct ovh_ctx {
   int device = 0;
   uint32_t flags = 0;
   hipStream_t stream = nullptr;
-  // pipelined batches (ovh_verify_batch_device_async): the final check + bisection of batch k
-  // run on a final stream while batch k + 1's per-vote stages run on stream; OVH_BATCH_SLOTS
-  // slots of batch state rotate (a slot is reused only after its final-stream work finished).
-  // Batches alternate between two final streams, so two finals may run at once (each shares a
-  // SIMD with a vote wave and takes longer than a vote kernel there).
+  // pipelined batches (ovh_verify_batch_device_async): the per-vote work of every batch runs in
+  // the vote pool (pool_st, high priority); batch k's fold levels, MSM, final check and bisection
+  // on a final stream (lowest priority) while later batches' votes run. OVH_BATCH_SLOTS slots of
+  // batch state rotate (a slot is reused only after its final-stream work finished). Batches
+  // alternate between two final streams, so two finals may run at once.
   hipStream_t fstream = nullptr, fstream2 = nullptr;
-  // OVH_NFIN=4: the batches' combined checks rotate over four final streams (A/B: with the
-  // pipelined pair 1,219k verifs/s against 1,266k on two, r04t)
-  hipStream_t fstream3 = nullptr, fstream4 = nullptr;
-  uint32_t nfin = 2;
   hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse; lazy)
   // ovh_verify_samemsg_device_async: [0], [1] the per-vote streams, in turn; [2] hash_to_G2 (lazy)
   hipStream_t vstream[3] = {};
-  // pipelined batches' per-vote stream pair (vote_pair; created with the context, before any
-  // lazily created stream, so each takes a hardware queue of its own)
-  hipStream_t pstream[3] = {};
-  uint32_t npair = 2;  // OVH_VOTE_PAIR=3: three per-vote streams in turn, =1: one (A/B)
+  // the vote pool (k_vm_pool): its two streams (created with the context, high priority), the
+  // device queue (PQ_WORDS words), the published batches' descriptors (one per slot), the
+  // workgroups' spill scratch (2 x pool_wgs x 4 x VOTE_NSCR entries: one area per pool stream),
+  // the grid size, the next batch's sequence number, and the timeout flag of k_pool_wait
+  // (coherent host memory)
+  hipStream_t pool_st[2] = {};  // every batch has a pool grid on each (see batch_front)
+  hipStream_t ann_st = nullptr;  // the batches' announcements (batch_front)
+  uint64_t* pool_q = nullptr;
+  void* pool_desc = nullptr;
+  uint32_t* pool_scr = nullptr;
+  uint32_t pool_wgs = 0;
+  uint64_t pool_seq = 0;
+  uint32_t* pool_err = nullptr;
   hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
+  // per slot: the state slab, the fold regions R0..R3 (R1: the 16-vote groups) and the pool's
+  // staged inputs -- views into one allocation each (slot k at k x the stride: PoolArgs)
   uint32_t* state_slot[OVH_BATCH_SLOTS] = {};
-  uint32_t* vscr[OVH_BATCH_SLOTS] = {};  // the spilled vote programs' per-vote scratch (VOTE_NSCR entries)
-  uint32_t* red_slot[OVH_BATCH_SLOTS] = {};  // fold regions R0..R3 (R1: the 16-vote groups)
+  uint32_t* red_slot[OVH_BATCH_SLOTS] = {};
+  uint32_t *state_all = nullptr, *red_all = nullptr;
+  uint8_t* pstage_all = nullptr;
+  size_t state_w = 0, red_w = 0, pstage_b = 0;
   int32_t* grp_ok[OVH_BATCH_SLOTS] = {};
   uint32_t slot_n[OVH_BATCH_SLOTS] = {};
   uint32_t* fin = nullptr;  // OVH_BATCH_SLOTS x FIN_STRIDE words: per-slot combine scratch
   uint32_t pipe_k = 0;
   int last_slot = 0;
-  // pipeline placement (environment OVH_FOLD_SIDE, read at ovh_create): 1 (default) runs the
-  // fold levels on the final stream instead of between two vote kernels on the main stream
-  bool fold_side = true;
   // batches of 2 .. small_max votes checked alone run the small-batch path (verify_small_locked);
   // OVH_SMALL_MAX=0 turns it off (A/B builds and tests of the standard path)
   uint32_t small_max = SMALL_MAX;
@@ -2010,9 +2241,6 @@ struct ovh_ctx {
   uint32_t comb_cap = 0;
   uint32_t* part_out = nullptr;  // multi-device: this device's partials (ring slot x {table, other votes} x 216 words)
   int32_t* result = nullptr;     // device verdict words
-  unsigned long long* vstart = nullptr;  // vote workgroups started (k_gate), device
-  uint64_t vlaunched = 0;                // vote workgroups launched, host
-  uint32_t wg_cap = 1024;                // vote workgroups resident at once (4 per CU)
   uint32_t last_n = 0;
   // RLC coefficients: fresh getrandom seed per batch, or the test seed (OVH_FLAG_TEST_RLC)
   uint64_t test_seed = 0, test_base = 0;
@@ -2053,24 +2281,8 @@ struct ovh_ctx {
   // 0: off; 1 (default): batches above small_max votes (below it the small-batch path has the
   // lower latency); 2: every batch with at most n / 2 distinct hashes
   int samemsg = 1;
-  // pipelined batches (ovh_verify_batch_device_async): consecutive batches' hash_to_field + vote
-  // kernels on the two per-vote streams in turn, so two batches' vote grids co-reside (the
-  // spilled vote program's LDS fits seven workgroups per CU); OVH_VOTE_PAIR=0: all on `stream`
-  bool vote_pair = VOTE_NSCR > 0;
-  bool gate = true;  // the final streams' residency gate (k_gate); OVH_GATE=0 drops it (A/B)
-  // pair_sync (OVH_PAIR_SYNC=1, A/B): a batch's vote grid waits for the next batch, and the two
-  // grids start together, one per stream of the pair (their inputs are staged per slot at the
-  // call, so the caller may reuse its buffers at once); a lone pending batch is launched by the
-  // next slot taken, any synchronisation or ovh_batch_wait. r04an: 1,276k verifs/s against
-  // 1,280k free-running -- the grids were not losing to a staggered start; off by default
-  bool pair_sync = false;
-  struct {
-    bool on = false;
-    int slot = 0;
-    uint32_t n = 0;
-    int32_t* codes = nullptr;
-  } pend;
-  uint8_t* pstage[OVH_BATCH_SLOTS] = {};  // staged sigs | pks of a pending / paired batch
+  // a pool batch's signatures | keys | table indices, staged per slot (k_pool_stage; views)
+  uint8_t* pstage[OVH_BATCH_SLOTS] = {};
   uint64_t sm_batches = 0, sm_votes = 0, sm_hashes = 0;
   // ovh_verify_samemsg_device_async: the one-hash plan of sm1_n votes (gid = 0 | head 0 | pairs)
   // and its level offsets; the hash of each slot (32 B per slot)
@@ -2170,8 +2382,20 @@ static_assert(LDS_GFIN + 16 <= 64 * 1024, "gfin LDS");
 // a CU holds its four vote workgroups beside the two finals that may be in flight (1 KiB
 // allocation granules assumed)
 constexpr size_t lds_granule(size_t b) { return (b + 1023) / 1024 * 1024; }
-static_assert(4 * lds_granule(LDS_VOTE > LDS_VOTE_T ? LDS_VOTE : LDS_VOTE_T) + 2 * lds_granule(LDS_FINAL) <= 160 * 1024,
-              "four vote workgroups + two finals per CU");
+// the vote pool: eight workgroups per CU (constants + four slices of the larger slot file)
+static constexpr size_t LDS_POOL = LDS_VOTE > LDS_VOTE_T ? LDS_VOTE : LDS_VOTE_T;
+static_assert(8 * lds_granule(LDS_POOL) <= 160 * 1024, "eight pool workgroups per CU");
+static_assert(VOTE_NSCR <= 4096 && VM_VOTE_NSLOTS <= 2048 && VM_VOTE_T_NSLOTS <= 2048,
+              "side words: 12-bit scratch entries, 11-bit slots (fpvm.hpp side_spill)");
+// pool workgroups left out per eight CUs (their places hold the final streams' kernels and
+// hash_to_field beside the pool), and the largest pool grid (the scratch is sized by it)
+// r05m (bench, 20 batches): 2 holes per 8 CUs 198k verifs/s, 4 373k, 8 (one place per CU)
+// 1,325k -- with fewer, the side kernels wait, the next batch's publication with them, and the
+// pool idles
+#ifndef POOL_HOLES_PER_8CU
+#define POOL_HOLES_PER_8CU 8u
+#endif
+#define POOL_MAX_WGS 4096u
 static_assert(FOLD_STRIDE_W <= VM_SLICES * VOTE_STRIDE_W && FOLD_STRIDE_W <= VM_SLICES * VOTE_T_STRIDE_W,
               "fused fold reuses the vote slots");
 
@@ -2303,9 +2527,8 @@ static int vm_init(ovh_ctx* c) {
   UPLOAD_HDBL(3, 8);
   UPLOAD_HDBL(4, 16);
 #undef UPLOAD_HDBL
-  HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE));
+  HIPCHK(hipFuncSetAttribute((const void*)k_vm_pool, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_POOL));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_signg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_SIGNG));
-  HIPCHK(hipFuncSetAttribute((const void*)k_vm_vote_t, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_VOTE_T));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold<VM_FOLD_UNITS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)LDS_FOLD));
   HIPCHK(hipFuncSetAttribute((const void*)k_vm_fold<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_FOLD1));
@@ -2343,15 +2566,15 @@ static Slab region_S(ovh_ctx* c, int slot, int r) {
               c->red_cap};
 }
 
-static int pair_flush(ovh_ctx* c);
-
+// Every stream of the context idle; OVH_ERR_DEVICE when a final stream gave up waiting for the
+// vote pool (k_pool_wait: its batch's results are not trustworthy).
 static int sync_all(ovh_ctx* c) {
-  CHK(pair_flush(c));  // a batch waiting for its pair partner is launched first
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->fstream));
   HIPCHK(hipStreamSynchronize(c->fstream2));
-  for (hipStream_t s : {c->fstream3, c->fstream4, c->pstream[0], c->pstream[1], c->pstream[2]})
+  for (hipStream_t s : {c->pool_st[0], c->pool_st[1], c->ann_st, c->vstream[0], c->vstream[1], c->vstream[2]})
     if (s) HIPCHK(hipStreamSynchronize(s));
+  if (c->pool_err && __atomic_load_n(c->pool_err, __ATOMIC_ACQUIRE)) return OVH_ERR_DEVICE;
   return 0;
 }
 
@@ -2397,24 +2620,32 @@ static int ensure_cap(ovh_ctx* c, size_t n) {
   while (cap < n) cap <<= 1;
   CHK(sync_all(c));
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
-    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
-                    (void*)c->vscr[k], (void*)c->pstage[k]})
+    for (void* p : {(void*)c->grp_ok[k], (void*)c->msm_buf[k]})
       if (p) (void)hipFree(p);
-    c->state_slot[k] = c->red_slot[k] = c->msm_buf[k] = c->vscr[k] = nullptr;
+    c->state_slot[k] = c->red_slot[k] = c->msm_buf[k] = nullptr;
     c->pstage[k] = nullptr;
     c->grp_ok[k] = nullptr;
     c->slot_n[k] = 0;
   }
+  for (void* p : {(void*)c->state_all, (void*)c->red_all, (void*)c->pstage_all})
+    if (p) (void)hipFree(p);
+  c->state_all = c->red_all = nullptr;
+  c->pstage_all = nullptr;
   c->last_n = 0;
   c->cap = 0;
   c->red_cap = cap / 4 > 64 ? cap / 4 : 64;
+  c->state_w = (size_t)S_TOTAL * 12 * cap;
+  c->red_w = (size_t)4 * PART_PLANES * 12 * c->red_cap;
+  c->pstage_b = ((size_t)cap * 148 + 255) / 256 * 256;
+  HIPCHK(hipMalloc(&c->state_all, c->state_w * 4 * OVH_BATCH_SLOTS));
+  HIPCHK(hipMalloc(&c->red_all, c->red_w * 4 * OVH_BATCH_SLOTS));
+  HIPCHK(hipMalloc(&c->pstage_all, c->pstage_b * OVH_BATCH_SLOTS));
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k) {
-    HIPCHK(hipMalloc(&c->state_slot[k], (size_t)S_TOTAL * 12 * cap * 4));
-    HIPCHK(hipMalloc(&c->red_slot[k], (size_t)4 * PART_PLANES * 12 * c->red_cap * 4));
+    c->state_slot[k] = c->state_all + k * c->state_w;
+    c->red_slot[k] = c->red_all + k * c->red_w;
+    c->pstage[k] = c->pstage_all + k * c->pstage_b;
     HIPCHK(hipMalloc(&c->grp_ok[k], ((size_t)cap / GROUP_VOTES + 1) * 4));
     HIPCHK(hipMalloc(&c->msm_buf[k], msm_words(cap) * 4));
-    if (VOTE_NSCR) HIPCHK(hipMalloc(&c->vscr[k], (size_t)cap * VOTE_NSCR * 12 * 4));
-    if (c->vote_pair) HIPCHK(hipMalloc(&c->pstage[k], (size_t)cap * 144));
   }
   c->cap = cap;
   return 0;
@@ -2454,12 +2685,10 @@ static int ensure_in(ovh_ctx* c, size_t bytes) {
 
 // Batch state slot k for the next batch on the main stream: the stream first waits until the
 // final stream has finished with the slot's previous batch (its bisection reads that state).
-static int take_slot(ovh_ctx* c, int* slot, bool keep_pending = false) {
-  if (!keep_pending) CHK(pair_flush(c));  // its slot must be in flight before the ring moves on
+static int take_slot(ovh_ctx* c, int* slot) {
   const int k = (int)(c->pipe_k % OVH_BATCH_SLOTS);
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_back[k], 0));
-  const uint32_t q = c->pipe_k % c->nfin;
-  c->fs[k] = q == 0 ? c->fstream : q == 1 ? c->fstream2 : q == 2 ? c->fstream3 : c->fstream4;
+  c->fs[k] = (c->pipe_k & 1) ? c->fstream2 : c->fstream;
   ++c->pipe_k;
   c->last_slot = k;
   *slot = k;
@@ -2495,20 +2724,18 @@ struct KeySrc {
   PkSrc pts;
 };
 
-// Per-vote stages of a batch in `slot`: hash_to_field, the vote kernel with fold level 0 fused
-// (-> R0), fold level 1 (-> R1: one partial per 16-vote group). alone: the batch's combined
-// check covers only this batch (not a shard of a larger combined check).
-static int batch_vote(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, KeySrc key, int32_t* d_codes,
-                      bool fold1, hipStream_t st);
+static uint32_t groups_of(uint32_t n) { return (n + GROUP_VOTES - 1) / GROUP_VOTES; }
 
+// Per-vote stages of a batch in `slot` (n >= 1 votes): on ovh_stream the staging of its
+// signatures and keys into the slot (k_pool_stage: the caller's buffers are then free in
+// ovh_stream order) and hash_to_field, then its publication to the vote pool and, on the pool
+// stream, a pool grid ("Vote pool"): the pool writes the codes, the state
+// planes and the fold level-0 partials (R0) and counts the batch's quads done. ev_front[slot] is
+// recorded after the publication (pool_join's stream waits for it). alone: the batch's combined
+// check covers only this batch (not a shard of a larger combined check).
 static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
-                       int32_t* d_codes, bool fold1 = true, bool alone = false, hipStream_t vst = nullptr,
-                       bool launch_vote = true) {
+                       int32_t* d_codes, bool alone = false) {
   Slab s{c->state_slot[slot], c->cap};
-  hipStream_t st = vst ? vst : c->stream;
-  // with a per-vote stream of the pair: hash_to_field on `stream` (after the caller's work and
-  // the slot's release), the per-vote stream waits for it -- so the pair stream runs its vote
-  // kernels back to back
   c->ev_mask = 0;
   uint64_t seed, base;
   CHK(draw_seed(c, &seed, &base));
@@ -2518,58 +2745,104 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   if (n == 1 && alone) base = UNIT_BASE;
   c->slot_seed[slot] = seed;
   c->slot_base[slot] = base;
-  {  // hash_to_field on the main stream: its inputs are ready in that stream's order (the
-     // staging copies, or a caller's writes on ovh_stream)
+  uint8_t* ps = c->pstage[slot];
+  const bool table = key.bytes == nullptr;
+  const uint64_t seq = c->pool_seq++;
+  // announced now, on a stream of its own: the batch may wait on ovh_stream for its slot
+  // (take_slot) while the pool drains the batches before it -- r05n: announced only in
+  // ovh_stream order, the pool ran dry behind a slot wait and its workgroups left (1,041k)
+  if (hipStreamWriteValue64(c->ann_st, c->pool_q + PQ_NANN, seq + 1, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    k_pool_announce<<<1, 64, 0, c->ann_st>>>(c->pool_q, seq + 1);
+  }
+  {
     StageScope p(c, ST_H2F, c->stream);
+    const uint32_t bytes = n * (table ? 96u : 144u) + (table && key.pts.idx ? n * 4u : 0u);
+    k_pool_stage<<<std::min(1024u, (bytes + 16 * WG - 1) / (16 * WG)), WG, 0, c->stream>>>(
+        n, d_sigs, key.bytes, table ? key.pts.idx : nullptr, ps);
     k_h2f<<<nblk(n), WG, 0, c->stream>>>(n, d_hashes, c->xmd, s);
   }
-  if (st != c->stream || !launch_vote) {
-    HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
-    if (launch_vote) HIPCHK(hipStreamWaitEvent(st, c->ev_front[slot], 0));
-  }
+  PoolBatch b{};
+  b.n = n;
+  b.nq = (n + VM_SLICES - 1) / VM_SLICES;
+  b.table = table;
+  b.has_idx = table && key.pts.idx;
+  b.seed = seed;
+  b.base = base;
+  b.codes = d_codes;
+  b.planes = key.pts.planes;
+  b.flags = key.pts.flags;
+  b.pcap = key.pts.cap;
+  b.state = s.p;
+  b.cap = s.cap;
+  const Slab r0 = region_F(c, slot, 0);
+  b.part0 = r0.p;
+  b.part_cap = r0.cap;
+  b.stage = ps;
+  b.clk = table ? c->vm_vote_t.clk : c->vm_vote.clk;
+  k_pool_publish<<<1, 64, 0, c->stream>>>(b, (uint32_t)slot, seq, c->pool_q, (PoolBatch*)c->pool_desc);
+  HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
   c->slot_n[slot] = n;
   c->last_n = n;
-  if (!launch_vote) return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
-  return batch_vote(c, slot, n, d_sigs, key, d_codes, fold1, st);
-}
-
-// The vote kernel of the batch in `slot` on stream st (its hash_to_field done in st's order),
-// then fold level 1 when fold1.
-static int batch_vote(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, KeySrc key, int32_t* d_codes,
-                      bool fold1, hipStream_t st) {
-  Slab s{c->state_slot[slot], c->cap};
-  const uint64_t seed = c->slot_seed[slot], base = c->slot_base[slot];
-  const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
+  // the batch's pool grids: one on each pool stream, each with half of the pool's places. A grid
+  // queued behind a running one on its stream starts only once that one's last workgroup has
+  // exited, so with one stream the workgroups that left during a gap in the queue were not
+  // replaced while the rest kept the grid alive (r05k); with a grid per stream per batch the pool
+  // refills from the next batch's grids, and a batch alone still gets every place
   const bool vev = (c->flags & OVH_FLAG_PROFILE) != 0;
   const uint32_t vk = c->vev_n % ovh_ctx::VEV_CAP;
-  if (vev) HIPCHK(hipEventRecord(c->vev0[vk], st));
-  {
-    StageScope p(c, ST_VOTE, st);
-    if (key.bytes)
-      k_vm_vote<<<nwg, 64, LDS_VOTE, st>>>(n, c->vm_vote, c->vm_fold, c->vm_consts, key.bytes, d_sigs, s, seed, base,
-                                           d_codes, region_F(c, slot, 0), c->gate ? c->vstart : nullptr, c->vscr[slot]);
-    else
-      k_vm_vote_t<<<nwg, 64, LDS_VOTE_T, st>>>(n, c->vm_vote_t, c->vm_fold, c->vm_consts, key.pts, d_sigs, s, seed,
-                                               base, d_codes, region_F(c, slot, 0), c->gate ? c->vstart : nullptr, c->vscr[slot]);
-    c->vlaunched += nwg;
-    c->clk_wgs = nwg < VM_CLOCK_WGS ? nwg : VM_CLOCK_WGS;
-    c->clk_table = key.bytes == nullptr;
+  PoolArgs pa;
+  pa.q = c->pool_q;
+  pa.descs = (const PoolBatch*)c->pool_desc;
+  pa.pv_code = c->vm_vote.code;
+  pa.pv_side = c->vm_vote.side;
+  pa.pt_code = c->vm_vote_t.code;
+  pa.pt_side = c->vm_vote_t.side;
+  pa.fold_code = c->vm_fold.code;
+  pa.cst = c->vm_consts;
+  for (uint32_t par = 0; par < 2; ++par) {
+    hipStream_t pst = c->pool_st[par];
+    HIPCHK(hipStreamWaitEvent(pst, c->ev_front[slot], 0));
+    if (par == 0) {  // the vote stage's and the vote spans' start (stream 0), end (stream 1)
+      if (c->flags & OVH_FLAG_PROFILE) HIPCHK(hipEventRecord(c->ev0[ST_VOTE], pst));
+      if (vev) HIPCHK(hipEventRecord(c->vev0[vk], pst));
+    }
+    pa.scr = c->pool_scr + (size_t)par * c->pool_wgs * VM_SLICES * VOTE_NSCR * 12;
+    k_vm_pool<<<c->pool_wgs, 64, LDS_POOL, pst>>>(pa);
+    if (par == 1) {
+      if (c->flags & OVH_FLAG_PROFILE) {
+        HIPCHK(hipEventRecord(c->ev1[ST_VOTE], pst));
+        c->ev_mask |= 1u << ST_VOTE;
+      }
+      if (vev) {
+        HIPCHK(hipEventRecord(c->vev1[vk], pst));
+        ++c->vev_n;
+      }
+    }
   }
-  if (vev) {
-    HIPCHK(hipEventRecord(c->vev1[vk], st));
-    ++c->vev_n;
-  }
-  if (fold1) {  // fold level 1: R0 -> R1 (one partial per 16-vote group)
-    StageScope p(c, ST_FOLD, st);
-    const uint32_t m1 = (nwg + 3) / 4;
-    k_vm_fold<VM_FOLD_UNITS><<<(m1 + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, st>>>(
-        nwg, c->vm_fold, c->vm_consts, region_F(c, slot, 0), region_S(c, slot, 0), region_F(c, slot, 1), nullptr);
-  }
+  c->clk_table = table;
+  c->clk_wgs = c->pool_wgs < VM_CLOCK_WGS ? c->pool_wgs : VM_CLOCK_WGS;
   HIPCHK(hipGetLastError());
   return 0;
 }
 
-static uint32_t groups_of(uint32_t n) { return (n + GROUP_VOTES - 1) / GROUP_VOTES; }
+// Timeout of a final stream's wait for the pool (k_pool_wait): far above any real batch -- the
+// pool may still be working through the OVH_BATCH_SLOTS - 1 batches published before this one.
+static uint64_t pool_wait_ticks(uint32_t n) { return 100000000ull * 4 + (uint64_t)n * 100 * OVH_BATCH_SLOTS; }
+
+// On stream st (after ev_front[slot]): wait for the pool to finish the batch in `slot`, then fold
+// level 1 (R0 -> R1: one partial per 16-vote group). *reg = 1, *m = the groups.
+static int pool_join(ovh_ctx* c, int slot, hipStream_t st, int* reg, uint32_t* m) {
+  const uint32_t n = c->slot_n[slot], nq = (n + VM_SLICES - 1) / VM_SLICES;
+  k_pool_wait<<<1, 64, 0, st>>>(c->pool_q, (uint32_t)slot, nq, pool_wait_ticks(n), c->pool_err);
+  *m = groups_of(n);
+  *reg = 1;
+  StageScope p(c, ST_FOLD, st);
+  k_vm_fold<1><<<*m, 64, LDS_FOLD1, st>>>(nq, c->vm_fold, c->vm_consts, region_F(c, slot, 0), region_S(c, slot, 0),
+                                           region_F(c, slot, 1), nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : OVH_ERR_DEVICE;
+}
+
 
 // Fold levels from region *reg (m partials) down to <= until, on stream st, alternating regions
 // R2 / R3 (R1 stays intact for the bisection). slices = 4 (main stream) or 1 (the final
@@ -2683,27 +2956,15 @@ static void enqueue_bisect(ovh_ctx* c, hipStream_t st, int slot, uint32_t n, int
                                          d_verdict, c->grp_ok[slot]);
 }
 
-// One batch, pipelined: per-vote stages + wide fold levels on the main stream; the narrow fold
-// levels, the combined check and the gated bisection on the final stream. Caller holds c->mu.
-// The final stream of `slot` after the vote kernel (batch_front without fold level 1): waits for
-// it, with `pipe` also for the next batch's vote workgroups to be resident (k_gate), then the
-// fold levels R0 -> R1 -> ... down to <= until partials (*reg, *m).
-static int side_front(ovh_ctx* c, int slot, uint32_t n, bool pipe, uint32_t until, int* reg, uint32_t* m,
-                      hipStream_t vst = nullptr) {
+// The final stream of `slot` after the batch's publication: waits for the pool (pool_join), then
+// the fold levels R0 -> R1 -> ... down to <= until partials (*reg, *m).
+static int side_front(ovh_ctx* c, int slot, uint32_t until, int* reg, uint32_t* m) {
   hipStream_t fst = c->fs[slot];
-  HIPCHK(hipEventRecord(c->ev_front[slot], vst ? vst : c->stream));
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
-  const uint32_t nwg = (n + VM_SLICES - 1) / VM_SLICES;
-  if (pipe && c->gate) k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
-  *m = groups_of(n);
-  *reg = 1;
-  k_vm_fold<VM_FOLD_UNITS><<<(*m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, fst>>>(
-      nwg, c->vm_fold, c->vm_consts, region_F(c, slot, 0), region_S(c, slot, 0), region_F(c, slot, 1), nullptr);
-  return fold_down(c, slot, fst, VM_SLICES, reg, m, until);
+  CHK(pool_join(c, slot, fst, reg, m));
+  return fold_down(c, slot, fst, 1, reg, m, until);
 }
 
-// pipe (ovh_verify_batch_device_async): the final stream first waits (k_gate) until the next
-// batch's vote workgroups are resident.
 // One standalone vote on the main stream (k_h2f, k_vm_vote1 / k_vm_vote_t1, k_vm_final1): its
 // own pairing equation, no coefficient (section 1 of DESIGN.md). Caller holds c->mu and waits.
 // h_host: the hash's host bytes, for the message cache (every vote of a round signs the same
@@ -2834,93 +3095,20 @@ static int verify_small_locked(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, co
   return 0;
 }
 
-// The back of a pipelined batch in `slot` whose hash_to_field ran on `stream` (ev_front[slot]):
-// its vote kernel on per-vote stream st (after `also`, when given), then the fold levels, MSM,
-// combined check and device-gated bisection on the slot's final stream.
-static int pair_back(ovh_ctx* c, int slot, uint32_t n, int32_t* d_codes, hipStream_t st, hipEvent_t also) {
-  HIPCHK(hipStreamWaitEvent(st, c->ev_front[slot], 0));
-  if (also) HIPCHK(hipStreamWaitEvent(st, also, 0));
-  const uint8_t* ps = c->pstage[slot];
-  CHK(batch_vote(c, slot, n, ps, KeySrc{ps + (size_t)n * 96, PkSrc{}}, d_codes, false, st));
+// One batch through the pool (or the small-batch path for 2 <= n <= small_max): per-vote stages
+// (batch_front), then on the slot's final stream the fold levels, the MSM, the combined check and
+// the device-gated bisection. Nothing waits on the host. Caller holds c->mu.
+static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
+                               int32_t* d_codes) {
+  CHK(ensure_cap(c, n));
+  if (n >= 2 && n <= c->small_max) return verify_small_locked(c, (uint32_t)n, d_sigs, d_hashes, key, d_codes);
+  int slot;
+  CHK(take_slot(c, &slot));
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, true));
   hipStream_t fst = c->fs[slot];
   uint32_t m;
   int reg;
-  CHK(side_front(c, slot, n, true, 4, &reg, &m, st));
-  int32_t* verdict = c->result + RES_BATCH + slot;
-  CHK(enqueue_msm(c, fst, slot, n, d_codes));
-  enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict, msm_S(c, slot));
-  enqueue_bisect(c, fst, slot, n, d_codes, verdict);
-  HIPCHK(hipEventRecord(c->ev_back[slot], fst));
-  HIPCHK(hipGetLastError());
-  return 0;
-}
-
-static int pair_flush(ovh_ctx* c) {
-  if (!c->pend.on) return 0;
-  c->pend.on = false;
-  return pair_back(c, c->pend.slot, c->pend.n, c->pend.codes, c->pstream[0], nullptr);
-}
-
-// pair_sync (ovh_verify_batch_device_async on the per-vote pair): stage the batch's signatures
-// and keys in its slot, run its hash_to_field; the first of two batches waits (pend), the second
-// launches both vote grids together -- one per stream of the pair, both after the second's
-// hash_to_field -- so they co-reside from their first workgroup to their last instead of
-// starting staggered behind each other's tails.
-static int verify_pair_locked(ovh_ctx* c, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
-                              const uint8_t* d_pks, int32_t* d_codes) {
-  int slot;
-  CHK(take_slot(c, &slot, true));
-  uint8_t* ps = c->pstage[slot];
-  HIPCHK(hipMemcpyAsync(ps, d_sigs, (size_t)n * 96, hipMemcpyDeviceToDevice, c->stream));
-  HIPCHK(hipMemcpyAsync(ps + (size_t)n * 96, d_pks, (size_t)n * 48, hipMemcpyDeviceToDevice, c->stream));
-  CHK(batch_front(c, slot, n, ps, d_hashes, KeySrc{ps + (size_t)n * 96, PkSrc{}}, d_codes, false, true, nullptr, false));
-  if (!c->pend.on) {
-    c->pend.on = true;
-    c->pend.slot = slot;
-    c->pend.n = n;
-    c->pend.codes = d_codes;
-    return 0;
-  }
-  const int ps0 = c->pend.slot;
-  const uint32_t n0 = c->pend.n;
-  int32_t* codes0 = c->pend.codes;
-  c->pend.on = false;
-  CHK(pair_back(c, ps0, n0, codes0, c->pstream[0], c->ev_front[slot]));
-  return pair_back(c, slot, n, d_codes, c->pstream[1], nullptr);
-}
-
-static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
-                               int32_t* d_codes, bool pipe = false) {
-  CHK(ensure_cap(c, n));
-  if (n >= 2 && n <= c->small_max) return verify_small_locked(c, (uint32_t)n, d_sigs, d_hashes, key, d_codes);
-  if (pipe && c->vote_pair && c->pair_sync && c->fold_side && key.bytes && c->pstage[0] && c->npair == 2)
-    return verify_pair_locked(c, (uint32_t)n, d_sigs, d_hashes, key.bytes, d_codes);
-  int slot;
-  CHK(take_slot(c, &slot));
-  const bool side = c->fold_side;
-  // pipelined: this batch's per-vote kernels on one of the two per-vote streams (vote_pair),
-  // after the caller's work on `stream` and the slot's release (take_slot)
-  hipStream_t vst = c->stream;
-  if (pipe && c->vote_pair) {
-    vst = c->pstream[slot % c->npair];
-  }
-  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, !side, true, vst));
-  hipStream_t fst = c->fs[slot];
-  uint32_t m = groups_of((uint32_t)n);
-  int reg = 1;
-  if (side) {  // fold levels on the final stream, beside the next batch's vote kernel
-    CHK(side_front(c, slot, (uint32_t)n, pipe, 4, &reg, &m, vst));
-  } else {
-    // every fold level on the main stream (it idles while a final runs): the final streams carry
-    // only the MSM, the finals and the bisections
-    CHK(fold_down(c, slot, vst, VM_SLICES, &reg, &m, 4));
-    HIPCHK(hipEventRecord(c->ev_front[slot], vst));
-    HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
-    if (pipe && c->gate) {
-      const uint32_t nwg = ((uint32_t)n + VM_SLICES - 1) / VM_SLICES;
-      k_gate<<<1, 64, 0, fst>>>(c->vstart, c->vlaunched + std::min(nwg, c->wg_cap), GATE_TICKS);
-    }
-  }
+  CHK(side_front(c, slot, 4, &reg, &m));
   int32_t* verdict = c->result + RES_BATCH + slot;
   CHK(enqueue_msm(c, fst, slot, (uint32_t)n, d_codes));
   enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict, msm_S(c, slot));
@@ -3115,7 +3303,7 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
     // high priority: that pool's four hardware queues hold only these three streams -- the
     // batch path's per-vote pair when the context has it (a fourth and fifth high-priority
     // stream shared queue 8 with the hash_to_G2 stream and serialised vsame behind it, r04ab)
-    hipStream_t* pair = c->pstream[0] ? c->pstream : c->vstream;
+    hipStream_t* pair = c->vstream;
     for (hipStream_t* v : {&pair[0], &pair[1]})
       if (!*v) {
         int lo = 0, hi = 0;
@@ -3277,8 +3465,9 @@ static int verify_host_locked(ovh_ctx* c, size_t n, const uint8_t* sigs, const u
 // Per-shard partial of `slot` (f folded to one, S from the MSM) -> AoS at `out` (device), on
 // the main stream.
 static int shard_partial(ovh_ctx* c, int slot, uint32_t n, const int32_t* d_codes, uint32_t* out, hipStream_t wait_on) {
-  uint32_t m = groups_of(n);
-  int reg = 1;
+  uint32_t m;
+  int reg;
+  CHK(pool_join(c, slot, c->stream, &reg, &m));
   CHK(fold_down(c, slot, c->stream, VM_SLICES, &reg, &m, 1));
   CHK(enqueue_msm(c, c->stream, slot, n, d_codes));
   if (wait_on) {  // the caller's earlier work on its stream (e.g. a gather reading `out`) first
@@ -3496,7 +3685,7 @@ static int submit_host_single(ovh_ctx* c, size_t n, const uint8_t* sigs, const u
     for (int part = 0; part < 2; ++part) {  // table votes [0, t), then the others [t, n)
       const size_t lo = part ? t : 0, cnt = part ? n - t : t;
       if (!cnt) continue;
-      CHK(verify_async_locked(c, cnt, in + 96 * lo, in + n * 96 + 32 * lo, staged_key(c, n, in, t, lo), dc + lo, true));
+      CHK(verify_async_locked(c, cnt, in + 96 * lo, in + n * 96 + 32 * lo, staged_key(c, n, in, t, lo), dc + lo));
       if (prev >= 0) HIPCHK(hipStreamWaitEvent(c->fs[c->last_slot], c->ev_back[prev], 0));
       prev = c->last_slot;
       last = c->fs[c->last_slot];
@@ -3562,11 +3751,11 @@ static int submit_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
       CHK(take_slot(s, &slot));
       s->test_base = root->test_base + lo + plo;  // OVH_FLAG_TEST_RLC only: one global index per vote
       CHK(batch_front(s, slot, (uint32_t)pc, in + 96 * plo, in + cnt * 96 + 32 * plo, staged_key(s, cnt, in, t, plo),
-                      dcodes + plo, false));
+                      dcodes + plo));
       const hipStream_t fst = s->fs[slot];
       int reg;
       uint32_t m;
-      CHK(side_front(s, slot, (uint32_t)pc, true, 1, &reg, &m));
+      CHK(side_front(s, slot, 1, &reg, &m));
       CHK(enqueue_msm(s, fst, slot, (uint32_t)pc, dcodes + plo));
       uint32_t* po = s->part_out + ((size_t)j * 2 + pi) * (OVH_PARTIAL_BYTES / 4);
       k_pack_partial2<<<1, 64, 0, fst>>>(region_F(s, slot, reg), msm_S(s, slot), po);
@@ -3681,72 +3870,46 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   if (!c) return nullptr;
   c->device = device;
   c->flags = flags;
-  if (const char* e = getenv("OVH_FOLD_SIDE")) c->fold_side = atoi(e) != 0;
+  // the two environment knobs (DESIGN.md sections 3.2, 3.3): the small-batch threshold and the
+  // same-message routing
   if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
   if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e);
-  if (const char* e = getenv("OVH_GATE")) c->gate = atoi(e) != 0;
-  if (const char* e = getenv("OVH_PAIR_SYNC")) c->pair_sync = atoi(e) != 0;
-  if (const char* e = getenv("OVH_VOTE_PAIR")) {
-    c->vote_pair = atoi(e) != 0;
-    c->npair = atoi(e) >= 3 ? 3 : atoi(e) == 1 ? 1 : 2;
-  }
-  // A/B knobs of the pipelined pair: the pair's and the final streams'
-  // priorities (1: the pair high, the finals lowest -- r04r: 1,268k verifs/s; a normal-priority
-  // pair 1,256k, normal-priority finals 1,091k)
-  int pair_prio = 1, fin_prio = 1;
-  if (const char* e = getenv("OVH_PAIR_PRIO")) pair_prio = atoi(e);
-  if (const char* e = getenv("OVH_FINAL_LOW")) fin_prio = atoi(e);
-  if (const char* e = getenv("OVH_NFIN")) c->nfin = atoi(e) >= 4 ? 4 : 2;
   int ncu = 0;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
-    c->wg_cap = 4u * (uint32_t)ncu;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
+  // the pool: eight vote workgroups fit a CU (LDS); POOL_HOLES_PER_8CU of every eight CUs' 64
+  // places are left to the final streams' kernels (fold, MSM, final, bisection) and the staging
+  // and hash_to_field of the next batches, which would otherwise wait for the pool to drain. The
+  // pool's places are split between the grids of the two pool streams (batch_front), which run
+  // side by side: each grid holds half of them
+  c->pool_wgs = ((uint32_t)ncu * 8 - (uint32_t)ncu * POOL_HOLES_PER_8CU / 8) / 2;
+  if (c->pool_wgs > POOL_MAX_WGS) c->pool_wgs = POOL_MAX_WGS;
   if (!dst) {
     dst = DEFAULT_DST;
     dst_len = 43;
   }
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
-  // OVH_FIN_CUS=N (A/B): the final streams on N CUs spread over the device (CU mask), and with
-  // OVH_VOTE_EXCL=1 the per-vote pair on the others -- the final-stream kernels then take LDS
-  // only where no vote grid needs it
-  int fin_cus = 0, vote_excl = 0;
-  if (const char* e = getenv("OVH_FIN_CUS")) fin_cus = atoi(e);
-  if (const char* e = getenv("OVH_VOTE_EXCL")) vote_excl = atoi(e);
-  std::vector<uint32_t> fmask, vmask;
-  if (fin_cus > 0 && ncu > fin_cus) {
-    fmask.assign(((size_t)ncu + 31) / 32, 0u);
-    vmask.assign(fmask.size(), 0u);
-    for (int k = 0; k < ncu; ++k) vmask[k / 32] |= 1u << (k % 32);
-    const int step = ncu / fin_cus;
-    for (int j = 0; j < fin_cus; ++j) {
-      const int k = j * step;
-      fmask[k / 32] |= 1u << (k % 32);
-      vmask[k / 32] &= ~(1u << (k % 32));
-    }
-  }
-  auto mk = [&](hipStream_t* st, int prio, const std::vector<uint32_t>& mask) {
-    if (!mask.empty()) return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()) == hipSuccess;
-    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, prio) == hipSuccess;
-  };
-  const std::vector<uint32_t> none;
-  const std::vector<uint32_t>& pmask = vote_excl ? vmask : none;
+  // streams: ovh_stream (normal priority), two final streams (lowest), the pool stream (highest;
+  // created with the context, so it holds a hardware queue of its own)
   bool ok = xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            mk(&c->fstream, fin_prio ? lo : 0, fmask) && mk(&c->fstream2, fin_prio ? lo : 0, fmask) &&
-            (c->nfin < 4 ||
-             (hipStreamCreateWithPriority(&c->fstream3, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess &&
-              hipStreamCreateWithPriority(&c->fstream4, hipStreamNonBlocking, fin_prio ? lo : 0) == hipSuccess)) &&
-            (!c->vote_pair ||
-             (mk(&c->pstream[0], pair_prio ? hi : 0, pmask) && mk(&c->pstream[1], pair_prio ? hi : 0, pmask) &&
-              (c->npair < 3 ||
-               hipStreamCreateWithPriority(&c->pstream[2], hipStreamNonBlocking, pair_prio ? hi : 0) == hipSuccess))) &&
+            hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->pool_st[0], hipStreamNonBlocking, hi) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->pool_st[1], hipStreamNonBlocking, hi) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->ann_st, hipStreamNonBlocking) == hipSuccess &&
             hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&
-            hipMalloc(&c->vstart, 8) == hipSuccess && hipMemset(c->vstart, 0, 8) == hipSuccess &&
             hipMemset(c->result, 0, RES_WORDS * 4) == hipSuccess &&
+            hipMalloc(&c->pool_q, (size_t)PQ_WORDS * 8) == hipSuccess && hipMemset(c->pool_q, 0, (size_t)PQ_WORDS * 8) == hipSuccess &&
+            hipMalloc(&c->pool_desc, sizeof(PoolBatch) * OVH_BATCH_SLOTS) == hipSuccess &&
+            hipMemset(c->pool_desc, 0, sizeof(PoolBatch) * OVH_BATCH_SLOTS) == hipSuccess &&
+            hipMalloc(&c->pool_scr, (size_t)2 * c->pool_wgs * VM_SLICES * VOTE_NSCR * 48) == hipSuccess &&
+            hipHostMalloc((void**)&c->pool_err, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
-  // two finals in flight at most (LDS budget below: four vote workgroups and two finals fit a
-  // CU; r02i ran one final stream per slot and lost 2.4 ms in every third vote kernel to a
-  // workgroup that found no LDS beside two finals and a final-stream fold)
+  if (ok) *c->pool_err = 0;
+  ok = ok && hipDeviceSynchronize() == hipSuccess;  // the memsets above are done before any batch
+  // two finals in flight at most (the pool's holes hold them; r02i ran one final stream per slot
+  // and lost 2.4 ms in every third vote kernel to a workgroup that found no LDS beside them)
   for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k) c->fs[k] = c->fstream;
   for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k)
     ok = hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) == hipSuccess &&
@@ -3833,14 +3996,16 @@ int ovh_multi_peer_matrix(ovh_ctx* c, uint8_t* out, size_t cap) {
 static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->fstream4, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
-                         c->pstream[0], c->pstream[1], c->pstream[2]})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
+                        c->pool_st[1], c->ann_st})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
-    for (void* p : {(void*)c->state_slot[k], (void*)c->red_slot[k], (void*)c->grp_ok[k], (void*)c->msm_buf[k],
-                    (void*)c->gslab[k], (void*)c->vscr[k], (void*)c->pstage[k]})
+    for (void* p : {(void*)c->grp_ok[k], (void*)c->msm_buf[k], (void*)c->gslab[k]})
       if (p) (void)hipFree(p);
-  for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->vstart, (void*)c->vm_consts,
+  for (void* p : {(void*)c->state_all, (void*)c->red_all, (void*)c->pstage_all})
+    if (p) (void)hipFree(p);
+  for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->pool_q, (void*)c->pool_desc,
+                  (void*)c->pool_scr, (void*)c->vm_consts,
                   (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
                   (void*)c->tab.planes, (void*)c->tab.flags, (void*)c->qc_buf, (void*)c->qt_buf, (void*)c->hc_planes, (void*)c->hc_inf, (void*)c->gather,
                   (void*)c->mfin, (void*)c->sm1_plan, (void*)c->sm1_hash})
@@ -3867,9 +4032,10 @@ static void destroy_one(ovh_ctx* c) {
     if (c->vev1[k]) (void)hipEventDestroy(c->vev1[k]);
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->fstream4, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
-                         c->pstream[0], c->pstream[1], c->pstream[2]})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
+                        c->pool_st[1], c->ann_st})
     if (s) (void)hipStreamDestroy(s);
+  if (c->pool_err) (void)hipHostFree(c->pool_err);
   delete c;
 }
 
@@ -3882,66 +4048,53 @@ void ovh_destroy(ovh_ctx* c) {
 
 int ovh_device_count(ovh_ctx* c) { return !c ? 0 : c->sub.empty() ? 1 : (int)c->sub.size(); }
 
-// Diagnostics: occupancy A/B of a VM program. `prog` 0 = vsame (75 slots:
-// eight workgroups fit a CU's LDS), 1 = vote (159 slots: four); `reps` launches over n votes of
-// whatever the state slab holds (the programs are branch-free: the input values do not change
-// the work), all on the main stream (streams = 1: one launch after the other) or alternating over
-// the main and the side stream (streams = 2: two launches co-resident when the LDS allows: two
-// waves per SIMD). *ms = the wall time of the whole sequence (HIP events).
+// Diagnostics. prog 0: occupancy A/B of the vsame program -- `reps`
+// launches over n votes of zeros (the programs are branch-free: the input values do not change
+// the work), all on the main stream (streams = 1) or alternating over the main and the side
+// stream (streams = 2: two launches co-resident). prog 1: the vote pool alone -- `reps` batches
+// of n zero votes published back to back (staging, hash_to_field, publication; a slot is reused
+// once the pool finished its previous batch), no final-stream work; `streams` is ignored.
+// *ms = the wall time of the whole sequence (HIP events).
 int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams, float* ms) {
-  if (!c || !ms || n == 0 || n > (1u << 20) || reps < 1 || streams < 1 || streams > 4 || prog < 0 || prog > 1)
+  if (!c || !ms || n == 0 || n > (1u << 20) || reps < 1 || streams < 1 || streams > 2 || prog < 0 || prog > 1)
     return OVH_ERR_ARG;
   if (!c->sub.empty()) c = c->sub[0];
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
   CHK(ensure_cap(c, n));
-  CHK(ensure_in(c, n * 176 + 64));
+  CHK(ensure_in(c, n * 180 + 64));
   CHK(sync_all(c));
   if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-  // OVH_DIAG_KEEP_IN=1: keep the staged votes of a preceding ovh_verify_batch (real data: the
-  // VM's timing does not depend on it, its power draw may)
-  if (!(getenv("OVH_DIAG_KEEP_IN") && atoi(getenv("OVH_DIAG_KEEP_IN")) != 0))
-    HIPCHK(hipMemsetAsync(c->in_buf, 0, n * 176, c->stream));
+  HIPCHK(hipMemsetAsync(c->in_buf, 0, n * 180, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   const Slab s{c->state_slot[0], c->cap};
-  int32_t* dc = (int32_t*)(c->in_buf + n * 144);
+  int32_t* dc = (int32_t*)(c->in_buf + n * 176);
   const uint32_t N = (uint32_t)n;
-  const bool scr_alt = getenv("OVH_DIAG_SCR_ALT") && atoi(getenv("OVH_DIAG_SCR_ALT")) != 0;
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
   HIPCHK(hipEventCreate(&e1));
   HIPCHK(hipEventRecord(e0, c->stream));
   HIPCHK(hipStreamWaitEvent(c->xstream, e0, 0));
-  for (hipStream_t p : c->pstream)
-    if (p) HIPCHK(hipStreamWaitEvent(p, e0, 0));
   for (int r = 0; r < reps; ++r) {
-    // streams 3: every launch on pipelined pair stream 0; 4: the pair in turn; prog 1 with
-    // OVH_DIAG_SCR_ALT=1: consecutive launches use two slots' scratch (as two batches do)
-    hipStream_t st = (streams == 2 && (r & 1)) ? c->xstream : c->stream;
-    if (streams >= 3 && c->pstream[0]) st = c->pstream[streams == 4 ? (r & 1) : 0];
-    if (prog == 0)
+    if (prog == 0) {
+      hipStream_t st = (streams == 2 && (r & 1)) ? c->xstream : c->stream;
       k_vm_vsame<false><<<(N + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(N, 0, c->vm_vsame, c->vm_consts,
-                                                                               c->in_buf + n * 96, PkSrc{}, c->in_buf,
+                                                                               c->in_buf + n * 128, PkSrc{}, c->in_buf,
                                                                                s, 1, 0, dc);
-    else
-      k_vm_vote<<<(N + VM_SLICES - 1) / VM_SLICES, 64, LDS_VOTE, st>>>(N, c->vm_vote, c->vm_fold, c->vm_consts,
-                                                                      c->in_buf + n * 96, c->in_buf, s, 1, 0, dc,
-                                                                      region_F(c, 0, 0), nullptr,
-                                                                      c->vscr[scr_alt ? (r & 1) : 0]);
+    } else {
+      const int slot = r % OVH_BATCH_SLOTS;
+      if (r >= OVH_BATCH_SLOTS)
+        k_pool_wait<<<1, 64, 0, c->stream>>>(c->pool_q, (uint32_t)slot, (N + VM_SLICES - 1) / VM_SLICES,
+                                             pool_wait_ticks(N), c->pool_err);
+      CHK(batch_front(c, slot, N, c->in_buf, c->in_buf + n * 96, KeySrc{c->in_buf + n * 128, PkSrc{}}, dc));
+    }
   }
   HIPCHK(hipGetLastError());
-  if (prog == 1) {  // OVH_FLAG_VM_CLOCK: ovh_vm_clock reads the launches' per-workgroup stamps
-    const uint32_t nwg = (N + VM_SLICES - 1) / VM_SLICES;
-    c->clk_wgs = nwg < VM_CLOCK_WGS ? nwg : VM_CLOCK_WGS;
-    c->clk_table = false;
+  if (prog == 1) c->clk_wgs = c->pool_wgs < VM_CLOCK_WGS ? c->pool_wgs : VM_CLOCK_WGS;
+  for (hipStream_t p : {c->xstream, c->pool_st[0], c->pool_st[1]}) {
+    HIPCHK(hipEventRecord(e1, p));
+    HIPCHK(hipStreamWaitEvent(c->stream, e1, 0));
   }
-  HIPCHK(hipEventRecord(e1, c->xstream));
-  HIPCHK(hipStreamWaitEvent(c->stream, e1, 0));
-  for (hipStream_t p : c->pstream)
-    if (p) {
-      HIPCHK(hipEventRecord(e1, p));
-      HIPCHK(hipStreamWaitEvent(c->stream, e1, 0));
-    }
   HIPCHK(hipEventRecord(e1, c->stream));
   HIPCHK(hipEventSynchronize(e1));
   HIPCHK(hipEventElapsedTime(ms, e0, e1));
@@ -4824,7 +4977,7 @@ int ovh_verify_batch_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, c
   if (n == 0) return 0;
   std::lock_guard<std::mutex> g(c->mu);
   HIPCHK(hipSetDevice(c->device));
-  return verify_async_locked(c, n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, true);
+  return verify_async_locked(c, n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes);
 }
 
 int ovh_verify_samemsg_device_async(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const uint8_t* hash,
@@ -4941,20 +5094,17 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
   }
-  // pipelined: only hash_to_field + the vote kernel on the main stream; the fold levels, the MSM
-  // and the packing on the slot's final stream (behind the residency gate), which the caller's
-  // stream then waits for (its all-gather, then ovh_combine_partials_device_async). The inputs
-  // are read in ovh_stream order (include/ovhip.h): waiting on `stream` here would also wait for
-  // the previous batch's gather and combine queued there and serialise the pipeline (r03b: 1,062k
-  // -> 796k verifs/s at one rank).
-  // the vote kernels of consecutive shards on the per-vote stream pair (vote_pair), as in
-  // ovh_verify_batch_device_async
-  hipStream_t vst = c->vote_pair ? c->pstream[slot % c->npair] : nullptr;
-  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false, false, vst));
+  // pipelined: only the staging, hash_to_field and the publication on the main stream (the votes
+  // in the pool); the fold levels, the MSM and the packing on the slot's final stream, which the
+  // caller's stream then waits for (its all-gather, then ovh_combine_partials_device_async). The
+  // inputs are read in ovh_stream order (include/ovhip.h): waiting on `stream` here would also
+  // wait for the previous batch's gather and combine queued there and serialise the pipeline
+  // (r03b: 1,062k -> 796k verifs/s at one rank).
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes));
   hipStream_t fst = c->fs[slot];
   int reg;
   uint32_t m;
-  CHK(side_front(c, slot, (uint32_t)n, true, 1, &reg, &m, vst));
+  CHK(side_front(c, slot, 1, &reg, &m));
   CHK(enqueue_msm(c, fst, slot, (uint32_t)n, d_codes));
   HIPCHK(hipEventRecord(c->ev_x[0], st));  // the caller's earlier work (a gather out of d_partial)
   HIPCHK(hipStreamWaitEvent(fst, c->ev_x[0], 0));
