@@ -55,6 +55,7 @@ SIGNATURES = [
     ("ovh_stage_name", ctypes.c_char_p, [ctypes.c_int]),
     ("ovh_vm_trace", ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), _sz]),
     ("ovh_vm_clock", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), _sz]),
+    ("ovh_pool_log", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), _sz]),
     ("ovh_diag_vm_occupancy", ctypes.c_int, [_vp, ctypes.c_int, _sz, ctypes.c_int, ctypes.c_int,
                                              ctypes.POINTER(ctypes.c_float)]),
     ("ovh_sign_batch_device", ctypes.c_int, [_vp, _sz, _vp, _vp, _vp]),

@@ -200,6 +200,10 @@ __global__ __launch_bounds__(64) void k_msm_pair(uint32_t lv, VmDev prog, uint32
                          : MODE == MSM_TL                  ? MSM_NT * (MSM_TM >> lv)
                                                            : (MSM_NT >> lv);
   if (blockIdx.x * SL >= total) return;  // whole workgroup idle (empty upper tree levels)
+  // above the pool's waves (2), as k_vm_final: the MSM levels are the final stream's longest
+  // stretch beside the pool (r05y pool log: 1.7-2.9 ms against 0.67 alone). r05q: at 2 (with the
+  // final at 3) 1,432k verifs/s vs 1,131k-1,316k at 0; r05z: at 3, 1,389k-1,407k vs 1,378k-1,386k
+  __builtin_amdgcn_s_setprio(3);
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;

@@ -379,14 +379,18 @@ enum : uint32_t {
   PQ_NANN = 3 * POOL_QW,
   PQ_DONE = 4 * POOL_QW,
   PQ_CLAIM = PQ_DONE + OVH_BATCH_SLOTS * POOL_QW,
+  PQ_INFL = PQ_CLAIM + OVH_BATCH_SLOTS * POOL_QW,  // quads claimed and not yet done (all batches)
 };
-constexpr uint32_t PQ_WORDS = PQ_CLAIM + OVH_BATCH_SLOTS * POOL_QW;
+constexpr uint32_t PQ_WORDS = PQ_INFL + POOL_QW;
 static_assert(POOL_SEQR > OVH_BATCH_SLOTS && POOL_SEQR / 2 <= POOL_QW, "pool queue layout");
 // A workgroup that finds the queue empty polls it for POOL_IDLE_TICKS (20 us) before it exits --
 // or, while a batch is announced but not yet published (nann > npub: its staging and
-// hash_to_field are on ovh_stream), for up to POOL_WAIT_TICKS (20 ms). r05h: without the
-// announcement the first grid's spare workgroups left during the next batch's hash_to_field and
-// the pool ran the rest of the run on the 1,024 workgroups that had found a quad.
+// hash_to_field are on ovh_stream) or another workgroup still runs a quad (infl > 0: more batches
+// are likely on their way), for up to POOL_WAIT_TICKS (20 ms). A grid whose spare workgroups left
+// while the rest kept working holds its stream (the next batches' grids queue behind it), and the
+// pool ran on the 1,024 workgroups that had found a quad: r05h without the announcement; r05x
+// (pool log) with it, the host still enqueueing batch k's final stream 50 us after batch k's
+// publication, before it announced batch k + 1.
 #define POOL_IDLE_TICKS 2000ull
 #define POOL_WAIT_TICKS 2000000ull
 
@@ -405,7 +409,41 @@ struct PoolBatch {  // one published batch (written by k_pool_publish, read by t
   const uint8_t* stage;  // staged signatures | keys | table indices (k_pool_stage)
   uint64_t* clk;         // OVH_FLAG_VM_CLOCK: per-workgroup stamps, else null
   uint32_t part_cap, pad;
+  uint64_t* plog;        // OVH_FLAG_VM_CLOCK: this batch's pool-log record (ovh_pool_log), else null
 };
+
+// Pool log (OVH_FLAG_VM_CLOCK diagnostics, ovh_pool_log): a ring of PLOG_RING batch records of
+// PLOG_WORDS u64: [0..15] 100 MHz stamps of the batch's stream events (PLOG_EV_*) and its seq,
+// then per quad (< PLOG_QUADS) its start (bits 0..47) with the workgroup (bits 48..63) and end.
+#define PLOG_RING 64u
+#define PLOG_QUADS 1024u
+#define PLOG_WORDS (16u + 2u * PLOG_QUADS)
+// then per pool grid launch (a ring of PLOG_GRIDS) and workgroup (< PLOG_WGS): entry and exit
+// stamps, the quads it ran and how it left (1: idle with nothing announced, 2: POOL_WAIT_TICKS,
+// 3: the claim loop's bound)
+#define PLOG_GRIDS 64u
+#define PLOG_WGS 1024u
+#define PLOG_WG_WORDS 4u
+#define PLOG_GRID_BASE ((size_t)PLOG_RING * PLOG_WORDS)
+#define PLOG_TOTAL (PLOG_GRID_BASE + (size_t)PLOG_GRIDS * (4 + PLOG_WGS * PLOG_WG_WORDS))
+enum : uint32_t { PLOG_EV_PUB = 0, PLOG_EV_DONE = 1, PLOG_EV_FOLD = 2, PLOG_EV_MSM = 3, PLOG_EV_FINAL = 4,
+                  PLOG_EV_BACK = 5, PLOG_EV_SEQ = 15 };
+__global__ void k_grid_hdr(uint64_t* g, uint64_t seq, uint32_t par, uint32_t wgs) {
+  for (uint32_t k = threadIdx.x; k < PLOG_WGS * PLOG_WG_WORDS; k += blockDim.x) g[4 + k] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    g[0] = seq;
+    g[1] = par;
+    g[2] = wgs;
+    g[3] = __builtin_amdgcn_s_memrealtime();  // its launch point on the pool stream
+  }
+}
+__global__ void k_stamp(uint64_t* p, uint64_t v) {
+  if (threadIdx.x == 0) {
+    p[0] = __builtin_amdgcn_s_memrealtime();
+    if (v != ~0ull) p[PLOG_EV_SEQ] = v;
+  }
+}
 
 // The pool kernel's arguments: the queue, the descriptors, the two vote programs' instruction
 // and side-word streams, the fold program, the constant table and the spill scratch. Everything
@@ -420,6 +458,7 @@ struct PoolArgs {
   const uint4* fold_code;
   const uint32_t* cst;
   uint32_t* scr;  // VM_SLICES x VOTE_NSCR entries per workgroup
+  uint64_t* wlog;  // OVH_FLAG_VM_CLOCK: this grid's workgroup log (PLOG_WG_WORDS per workgroup), else null
 };
 
 __device__ __forceinline__ uint64_t* pq_done(uint64_t* q, uint32_t slot) { return q + PQ_DONE + slot * POOL_QW; }
@@ -449,8 +488,8 @@ __global__ __launch_bounds__(64) void k_pool_publish(PoolBatch b, uint32_t slot,
 }
 
 // Announce batch seq: nann = seq + 1 tells idle pool workgroups that a publication is on its way
-// (the announcement stream's write, when the host enqueues the batch; this kernel only if the
-// stream write is not available).
+// (pool_take_slot: on ovh_stream ahead of the slot wait, so the announcement of the next batch
+// follows the publication of the previous one and never waits for a slot).
 __global__ __launch_bounds__(64) void k_pool_announce(uint64_t* q, uint64_t n) {
   if (threadIdx.x == 0) __hip_atomic_store(q + PQ_NANN, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -482,14 +521,20 @@ __device__ __forceinline__ uint64_t qldu(const uint64_t* p) {
   const uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
 }
-__device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* slot_out, uint32_t* quad_out) {
+__device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* slot_out, uint32_t* quad_out,
+                               uint32_t* why) {
   uint64_t t0 = wclock();
+  *why = 3;
 #pragma unroll 1
   for (uint32_t tries = 0; tries < (1u << 22); ++tries) {
     const uint64_t s = qldu(q + PQ_CUR), np = qldu(q + PQ_NPUB);
     if (s >= np) {
       const uint64_t idle = wclock() - t0;
-      if (idle > POOL_WAIT_TICKS || (idle > POOL_IDLE_TICKS && qldu(q + PQ_NANN) <= np)) return 0;
+      if (idle > POOL_WAIT_TICKS ||
+          (idle > POOL_IDLE_TICKS && qldu(q + PQ_NANN) <= np && qldu(q + PQ_INFL) == 0)) {
+        *why = idle > POOL_WAIT_TICKS ? 2 : 1;
+        return 0;
+      }
       __builtin_amdgcn_s_sleep(8);
       continue;
     }
@@ -513,6 +558,7 @@ __device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* sl
     // (whoever wins; a claim that took exactly the last quad does not, the next claimer does)
     if (seq != s || !mine) lane0_cas(q + PQ_CUR, s, s + 1);
     if (mine) {
+      (void)lane0_fetch_add(q + PQ_INFL, 1ull);
       *slot_out = slot;
       *quad_out = idx;
       return 1;
@@ -584,6 +630,12 @@ __device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, u
     if (threadIdx.x == 0) {
       park[0] = slot_in;
       park[1] = quad_in;
+      if (dgetp(&bd->plog)) {
+        uint32_t* h3 = lds + SLOT_BASE_W + 3 * STRIDE + NSLOTS * 12 + 2;
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        h3[0] = (uint32_t)t;
+        h3[1] = (uint32_t)(t >> 32);
+      }
     }
     __syncthreads();
     if (active) {
@@ -680,7 +732,15 @@ __device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, u
   // the quad's codes, planes and partial, then its done count (k_pool_wait)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(pq_done(a.q, slot), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(pq_done(a.q, slot), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(a.q + PQ_INFL, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // - 1
+  }
+  if (uint64_t* pl = dgetp(&bd->plog); pl && threadIdx.x == 0 && quad < PLOG_QUADS) {
+    const uint32_t* h3 = lds + SLOT_BASE_W + 3 * STRIDE + NSLOTS * 12 + 2;
+    pl[16 + 2 * quad] = ((uint64_t)h3[0] | (uint64_t)(h3[1] & 0xFFFFu) << 32) | (uint64_t)(blockIdx.x & 0xFFFFu) << 48;
+    pl[16 + 2 * quad + 1] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // The pool: each workgroup claims quads until the queue stays empty (pool_claim), then exits.
@@ -688,20 +748,29 @@ __device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, u
 // workgroup's own spill area (4 x VOTE_NSCR entries), reused quad after quad. Two waves per SIMD
 // are declared (the register budget that makes two pool workgroups share a SIMD).
 __global__ __launch_bounds__(64, 2) void k_vm_pool(PoolArgs a) {
-  __builtin_amdgcn_s_setprio(2);  // per-vote work outranks a co-resident final-stream wave
+  __builtin_amdgcn_s_setprio(2);  // above the final streams' fold checks, below k_vm_final (3)
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   load_consts(lds, a.cst, VM_NCONST);
+  const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
   vote_stagger();
+  uint32_t nquads = 0, why = 0;
 #pragma unroll 1
-  for (;;) {
+  for (;; ++nquads) {
     uint32_t slot = 0, quad = 0;
-    if (!pool_claim(a.q, a.descs, &slot, &quad)) break;
+    if (!pool_claim(a.q, a.descs, &slot, &quad, &why)) break;
     slot = uni(slot);
     quad = uni(quad);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this batch's descriptor and inputs, fresh
     if (uni(dget(&a.descs[slot].table))) vote_quad<true>(a, slot, quad, lds);
     else vote_quad<false>(a, slot, quad, lds);
+  }
+  if (a.wlog && threadIdx.x == 0 && blockIdx.x < PLOG_WGS) {
+    uint64_t* w = a.wlog + (size_t)blockIdx.x * PLOG_WG_WORDS;
+    w[0] = t_in;
+    w[1] = __builtin_amdgcn_s_memrealtime();
+    w[2] = nquads;
+    w[3] = why;
   }
 }
 
@@ -745,7 +814,7 @@ __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const ui
                                                 Slab inS, Slab out, const int32_t* __restrict__ codes,
                                                 const int32_t* __restrict__ gate = nullptr) {
   if (gate && *gate == 1) return;
-  __builtin_amdgcn_s_setprio(2);  // short: run ahead of a co-resident final wave
+  __builtin_amdgcn_s_setprio(2);  // short, as the pool's waves
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -760,12 +829,12 @@ __global__ __launch_bounds__(64) void k_vm_fold(uint32_t m, VmDev prog, const ui
 
 // Final: prod F * Miller(-G1, sum S) over in[0..m-1] (m <= 4) -> FE == 1 -> *result.
 // xS.p: partial 0's S is xS[0] (the batch's MSM result; the folded partials carry S = O).
-#ifndef OVH_FINAL_PRIO
-#define OVH_FINAL_PRIO 0
-#endif
 __global__ __launch_bounds__(64) void k_vm_final(uint32_t m, VmDev prog, const uint32_t* __restrict__ cst_g, Slab inF,
                                                  Slab inS, Slab xS, int32_t* __restrict__ result) {
-  if (OVH_FINAL_PRIO) __builtin_amdgcn_s_setprio(OVH_FINAL_PRIO);
+  // above the pool's waves (2): the one-wave final shares its SIMD with a pool wave and ran
+  // 4.2 ms instead of 2.1 at equal or lower priority; its slot ran out first (r05p trace). With
+  // this and the MSM levels at 2: 1,432k verifs/s vs 1,131k-1,316k (r05q A/B)
+  __builtin_amdgcn_s_setprio(3);
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
@@ -2192,8 +2261,8 @@ struct ovh_ctx {
   // the vote pool (pool_st, high priority); batch k's fold levels, MSM, final check and bisection
   // on a final stream (lowest priority) while later batches' votes run. OVH_BATCH_SLOTS slots of
   // batch state rotate (a slot is reused only after its final-stream work finished). Batches
-  // alternate between two final streams, so two finals may run at once.
-  hipStream_t fstream = nullptr, fstream2 = nullptr;
+  // take the NFIN_STREAMS final streams in turn, so that many chains run at once.
+  hipStream_t fstream = nullptr, fstream2 = nullptr, fstream3 = nullptr;
   hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse; lazy)
   // ovh_verify_samemsg_device_async: [0], [1] the per-vote streams, in turn; [2] hash_to_G2 (lazy)
   hipStream_t vstream[3] = {};
@@ -2203,13 +2272,15 @@ struct ovh_ctx {
   // the grid size, the next batch's sequence number, and the timeout flag of k_pool_wait
   // (coherent host memory)
   hipStream_t pool_st[2] = {};  // every batch has a pool grid on each (see batch_front)
-  hipStream_t ann_st = nullptr;  // the batches' announcements (batch_front)
   uint64_t* pool_q = nullptr;
   void* pool_desc = nullptr;
   uint32_t* pool_scr = nullptr;
   uint32_t pool_wgs = 0;
   uint64_t pool_seq = 0;
   uint32_t* pool_err = nullptr;
+  uint64_t* plog = nullptr;  // OVH_FLAG_VM_CLOCK: the pool log (PLOG_RING records)
+  uint64_t plog_seq[OVH_BATCH_SLOTS] = {};  // the seq of the batch in each slot
+  uint64_t plog_grids = 0;
   hipStream_t fs[OVH_BATCH_SLOTS] = {};  // final stream of the batch in each slot (take_slot)
   hipEvent_t ev_front[OVH_BATCH_SLOTS] = {}, ev_back[OVH_BATCH_SLOTS] = {};
   hipEvent_t ev_x[4] = {};  // stream-order handoffs with a caller's stream / other devices
@@ -2395,6 +2466,10 @@ static_assert(VOTE_NSCR <= 4096 && VM_VOTE_NSLOTS <= 2048 && VM_VOTE_T_NSLOTS <=
 #ifndef POOL_HOLES_PER_8CU
 #define POOL_HOLES_PER_8CU 8u
 #endif
+// or: CUs kept from the pool streams (CU mask), the pool filling the others (8 per CU)
+#ifndef POOL_RESERVE_CUS
+#define POOL_RESERVE_CUS 0u
+#endif
 #define POOL_MAX_WGS 4096u
 static_assert(FOLD_STRIDE_W <= VM_SLICES * VOTE_STRIDE_W && FOLD_STRIDE_W <= VM_SLICES * VOTE_T_STRIDE_W,
               "fused fold reuses the vote slots");
@@ -2572,7 +2647,8 @@ static int sync_all(ovh_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->fstream));
   HIPCHK(hipStreamSynchronize(c->fstream2));
-  for (hipStream_t s : {c->pool_st[0], c->pool_st[1], c->ann_st, c->vstream[0], c->vstream[1], c->vstream[2]})
+  HIPCHK(hipStreamSynchronize(c->fstream3));
+  for (hipStream_t s : {c->pool_st[0], c->pool_st[1], c->vstream[0], c->vstream[1], c->vstream[2]})
     if (s) HIPCHK(hipStreamSynchronize(s));
   if (c->pool_err && __atomic_load_n(c->pool_err, __ATOMIC_ACQUIRE)) return OVH_ERR_DEVICE;
   return 0;
@@ -2685,14 +2761,30 @@ static int ensure_in(ovh_ctx* c, size_t bytes) {
 
 // Batch state slot k for the next batch on the main stream: the stream first waits until the
 // final stream has finished with the slot's previous batch (its bisection reads that state).
+// final streams: a batch's fold levels, MSM, final and bisection take 4-6 ms beside the pool
+// (r05y pool log), so two in turn held the pipeline to one batch per ~3 ms; three: 1,378k-1,386k
+// verifs/s vs 1,254k-1,260k (r05z)
+#define NFIN_STREAMS 3u
 static int take_slot(ovh_ctx* c, int* slot) {
   const int k = (int)(c->pipe_k % OVH_BATCH_SLOTS);
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_back[k], 0));
-  c->fs[k] = (c->pipe_k & 1) ? c->fstream2 : c->fstream;
+  const uint64_t f = c->pipe_k % NFIN_STREAMS;
+  c->fs[k] = f == 0 ? c->fstream : f == 1 ? c->fstream2 : c->fstream3;
   ++c->pipe_k;
   c->last_slot = k;
   *slot = k;
   return 0;
+}
+
+// take_slot for a batch the pool will run (batch_front): its announcement first, on ovh_stream
+// ahead of the slot wait. Idle pool workgroups stay while nann > npub (pool_claim); announced
+// behind the slot wait -- or on a stream of its own, whose hardware queue the runtime may share
+// with ovh_stream -- the next batch's announcement waited for a final stream, the spare
+// workgroups left, and the rest of the run had 1,024 of the pool's 1,792 (r05v pool log; the
+// slow mode of r05q-r05u, 3.9-4.0 ms per batch)
+static int pool_take_slot(ovh_ctx* c, int* slot) {
+  k_pool_announce<<<1, 64, 0, c->stream>>>(c->pool_q, c->pool_seq + 1);
+  return take_slot(c, slot);
 }
 
 // RLC coefficients of the next batch: SplitMix64(seed, base + i) with a fresh secret seed from
@@ -2748,13 +2840,6 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   uint8_t* ps = c->pstage[slot];
   const bool table = key.bytes == nullptr;
   const uint64_t seq = c->pool_seq++;
-  // announced now, on a stream of its own: the batch may wait on ovh_stream for its slot
-  // (take_slot) while the pool drains the batches before it -- r05n: announced only in
-  // ovh_stream order, the pool ran dry behind a slot wait and its workgroups left (1,041k)
-  if (hipStreamWriteValue64(c->ann_st, c->pool_q + PQ_NANN, seq + 1, 0) != hipSuccess) {
-    (void)hipGetLastError();
-    k_pool_announce<<<1, 64, 0, c->ann_st>>>(c->pool_q, seq + 1);
-  }
   {
     StageScope p(c, ST_H2F, c->stream);
     const uint32_t bytes = n * (table ? 96u : 144u) + (table && key.pts.idx ? n * 4u : 0u);
@@ -2780,7 +2865,10 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   b.part_cap = r0.cap;
   b.stage = ps;
   b.clk = table ? c->vm_vote_t.clk : c->vm_vote.clk;
+  b.plog = c->plog ? c->plog + (size_t)(seq % PLOG_RING) * PLOG_WORDS : nullptr;
+  c->plog_seq[slot] = seq;
   k_pool_publish<<<1, 64, 0, c->stream>>>(b, (uint32_t)slot, seq, c->pool_q, (PoolBatch*)c->pool_desc);
+  if (b.plog) k_stamp<<<1, 64, 0, c->stream>>>(b.plog + PLOG_EV_PUB, seq);
   HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));
   c->slot_n[slot] = n;
   c->last_n = n;
@@ -2808,6 +2896,12 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
       if (vev) HIPCHK(hipEventRecord(c->vev0[vk], pst));
     }
     pa.scr = c->pool_scr + (size_t)par * c->pool_wgs * VM_SLICES * VOTE_NSCR * 12;
+    pa.wlog = nullptr;
+    if (c->plog) {  // grid record: [seq, par, workgroups, -], then the workgroups'
+      uint64_t* g = c->plog + PLOG_GRID_BASE + (size_t)(c->plog_grids++ % PLOG_GRIDS) * (4 + PLOG_WGS * PLOG_WG_WORDS);
+      k_grid_hdr<<<1, 64, 0, pst>>>(g, seq, par, c->pool_wgs);
+      pa.wlog = g + 4;
+    }
     k_vm_pool<<<c->pool_wgs, 64, LDS_POOL, pst>>>(pa);
     if (par == 1) {
       if (c->flags & OVH_FLAG_PROFILE) {
@@ -2832,9 +2926,16 @@ static uint64_t pool_wait_ticks(uint32_t n) { return 100000000ull * 4 + (uint64_
 
 // On stream st (after ev_front[slot]): wait for the pool to finish the batch in `slot`, then fold
 // level 1 (R0 -> R1: one partial per 16-vote group). *reg = 1, *m = the groups.
+// OVH_FLAG_VM_CLOCK: a stamp of event ev of the batch in `slot` on stream st (the pool log)
+static void plog_stamp(ovh_ctx* c, int slot, uint32_t ev, hipStream_t st) {
+  if (c->plog)
+    k_stamp<<<1, 64, 0, st>>>(c->plog + (size_t)(c->plog_seq[slot] % PLOG_RING) * PLOG_WORDS + ev, ~0ull);
+}
+
 static int pool_join(ovh_ctx* c, int slot, hipStream_t st, int* reg, uint32_t* m) {
   const uint32_t n = c->slot_n[slot], nq = (n + VM_SLICES - 1) / VM_SLICES;
   k_pool_wait<<<1, 64, 0, st>>>(c->pool_q, (uint32_t)slot, nq, pool_wait_ticks(n), c->pool_err);
+  plog_stamp(c, slot, PLOG_EV_DONE, st);
   *m = groups_of(n);
   *reg = 1;
   StageScope p(c, ST_FOLD, st);
@@ -3103,16 +3204,20 @@ static int verify_async_locked(ovh_ctx* c, size_t n, const uint8_t* d_sigs, cons
   CHK(ensure_cap(c, n));
   if (n >= 2 && n <= c->small_max) return verify_small_locked(c, (uint32_t)n, d_sigs, d_hashes, key, d_codes);
   int slot;
-  CHK(take_slot(c, &slot));
+  CHK(pool_take_slot(c, &slot));
   CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, key, d_codes, true));
   hipStream_t fst = c->fs[slot];
   uint32_t m;
   int reg;
   CHK(side_front(c, slot, 4, &reg, &m));
+  plog_stamp(c, slot, PLOG_EV_FOLD, fst);
   int32_t* verdict = c->result + RES_BATCH + slot;
   CHK(enqueue_msm(c, fst, slot, (uint32_t)n, d_codes));
+  plog_stamp(c, slot, PLOG_EV_MSM, fst);
   enqueue_final(c, fst, region_F(c, slot, reg), region_S(c, slot, reg), m, verdict, msm_S(c, slot));
+  plog_stamp(c, slot, PLOG_EV_FINAL, fst);
   enqueue_bisect(c, fst, slot, (uint32_t)n, d_codes, verdict);
+  plog_stamp(c, slot, PLOG_EV_BACK, fst);
   HIPCHK(hipEventRecord(c->ev_back[slot], fst));
   HIPCHK(hipGetLastError());
   return 0;
@@ -3522,7 +3627,7 @@ static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
       const size_t plo = part ? t : 0, pc = part ? cnt - t : t;
       if (!pc) continue;
       Part p{0, plo, pc};
-      CHK(take_slot(s, &p.slot));
+      CHK(pool_take_slot(s, &p.slot));
       s->test_base = root->test_base + lo + plo;  // OVH_FLAG_TEST_RLC only: one global index per vote
       CHK(batch_front(s, p.slot, (uint32_t)pc, in + 96 * plo, in + cnt * 96 + 32 * plo, staged_key(s, cnt, in, t, plo),
                       dcodes[d] + plo));
@@ -3748,7 +3853,7 @@ static int submit_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
       const size_t plo = part ? t : 0, pc = part ? cnt - t : t;
       if (!pc) continue;
       int slot;
-      CHK(take_slot(s, &slot));
+      CHK(pool_take_slot(s, &slot));
       s->test_base = root->test_base + lo + plo;  // OVH_FLAG_TEST_RLC only: one global index per vote
       CHK(batch_front(s, slot, (uint32_t)pc, in + 96 * plo, in + cnt * 96 + 32 * plo, staged_key(s, cnt, in, t, plo),
                       dcodes + plo));
@@ -3882,6 +3987,19 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   // pool's places are split between the grids of the two pool streams (batch_front), which run
   // side by side: each grid holds half of them
   c->pool_wgs = ((uint32_t)ncu * 8 - (uint32_t)ncu * POOL_HOLES_PER_8CU / 8) / 2;
+  std::vector<uint32_t> pool_mask;
+  if (POOL_RESERVE_CUS > 0 && (uint32_t)ncu >= 8 * POOL_RESERVE_CUS) {
+    // reserved CU k: bit s k + k % 8 (s = ncu / reserve), so the reserved CUs spread over the
+    // XCDs whether the mask's bits run XCD by XCD or round-robin over them
+    const uint32_t st = (uint32_t)ncu / POOL_RESERVE_CUS;
+    pool_mask.assign(((uint32_t)ncu + 31) / 32, 0u);
+    for (uint32_t i = 0; i < (uint32_t)ncu; ++i) pool_mask[i / 32] |= 1u << (i % 32);
+    for (uint32_t k = 0; k < POOL_RESERVE_CUS; ++k) {
+      const uint32_t b = st * k + k % 8;
+      pool_mask[b / 32] &= ~(1u << (b % 32));
+    }
+    c->pool_wgs = ((uint32_t)ncu - POOL_RESERVE_CUS) * 8 / 2;
+  }
   if (c->pool_wgs > POOL_MAX_WGS) c->pool_wgs = POOL_MAX_WGS;
   if (!dst) {
     dst = DEFAULT_DST;
@@ -3889,15 +4007,20 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   }
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
-  // streams: ovh_stream (normal priority), two final streams (lowest), the pool stream (highest;
-  // created with the context, so it holds a hardware queue of its own)
+  // streams: ovh_stream (normal priority), three final streams (lowest), the two pool streams
+  // (highest; created with the context, so each holds a hardware queue of its own)
   bool ok = xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->pool_st[0], hipStreamNonBlocking, hi) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->pool_st[1], hipStreamNonBlocking, hi) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->ann_st, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream3, hipStreamNonBlocking, lo) == hipSuccess &&
+            (pool_mask.empty()
+                 ? hipStreamCreateWithPriority(&c->pool_st[0], hipStreamNonBlocking, hi) == hipSuccess &&
+                       hipStreamCreateWithPriority(&c->pool_st[1], hipStreamNonBlocking, hi) == hipSuccess
+                 : hipExtStreamCreateWithCUMask(&c->pool_st[0], (uint32_t)pool_mask.size(), pool_mask.data()) ==
+                           hipSuccess &&
+                       hipExtStreamCreateWithCUMask(&c->pool_st[1], (uint32_t)pool_mask.size(), pool_mask.data()) ==
+                           hipSuccess) &&
             hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&
             hipMemset(c->result, 0, RES_WORDS * 4) == hipSuccess &&
             hipMalloc(&c->pool_q, (size_t)PQ_WORDS * 8) == hipSuccess && hipMemset(c->pool_q, 0, (size_t)PQ_WORDS * 8) == hipSuccess &&
@@ -3907,9 +4030,12 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
             hipHostMalloc((void**)&c->pool_err, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
   if (ok) *c->pool_err = 0;
+  if (ok && (flags & OVH_FLAG_VM_CLOCK))
+    ok = hipMalloc(&c->plog, PLOG_TOTAL * 8) == hipSuccess && hipMemset(c->plog, 0, PLOG_TOTAL * 8) == hipSuccess;
   ok = ok && hipDeviceSynchronize() == hipSuccess;  // the memsets above are done before any batch
-  // two finals in flight at most (the pool's holes hold them; r02i ran one final stream per slot
-  // and lost 2.4 ms in every third vote kernel to a workgroup that found no LDS beside them)
+  // NFIN_STREAMS finals in flight at most (the pool's holes hold them; r02i ran one final stream
+  // per slot and lost 2.4 ms in every third vote kernel to a workgroup that found no LDS beside
+  // them)
   for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k) c->fs[k] = c->fstream;
   for (int k = 0; ok && k < OVH_BATCH_SLOTS; ++k)
     ok = hipEventCreateWithFlags(&c->ev_front[k], hipEventDisableTiming) == hipSuccess &&
@@ -3996,8 +4122,8 @@ int ovh_multi_peer_matrix(ovh_ctx* c, uint8_t* out, size_t cap) {
 static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
-                        c->pool_st[1], c->ann_st})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
+                        c->pool_st[1]})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->grp_ok[k], (void*)c->msm_buf[k], (void*)c->gslab[k]})
@@ -4005,7 +4131,7 @@ static void destroy_one(ovh_ctx* c) {
   for (void* p : {(void*)c->state_all, (void*)c->red_all, (void*)c->pstage_all})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->in_buf, (void*)c->part_out, (void*)c->result, (void*)c->pool_q, (void*)c->pool_desc,
-                  (void*)c->pool_scr, (void*)c->vm_consts,
+                  (void*)c->pool_scr, (void*)c->plog, (void*)c->vm_consts,
                   (void*)c->fin, (void*)c->scr, (void*)c->scr_pk, (void*)c->scr_sig, (void*)c->comb,
                   (void*)c->tab.planes, (void*)c->tab.flags, (void*)c->qc_buf, (void*)c->qt_buf, (void*)c->hc_planes, (void*)c->hc_inf, (void*)c->gather,
                   (void*)c->mfin, (void*)c->sm1_plan, (void*)c->sm1_hash})
@@ -4032,8 +4158,8 @@ static void destroy_one(ovh_ctx* c) {
     if (c->vev1[k]) (void)hipEventDestroy(c->vev1[k]);
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
-                        c->pool_st[1], c->ann_st})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
+                        c->pool_st[1]})
     if (s) (void)hipStreamDestroy(s);
   if (c->pool_err) (void)hipHostFree(c->pool_err);
   delete c;
@@ -4083,6 +4209,7 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
                                                                                s, 1, 0, dc);
     } else {
       const int slot = r % OVH_BATCH_SLOTS;
+      k_pool_announce<<<1, 64, 0, c->stream>>>(c->pool_q, c->pool_seq + 1);
       if (r >= OVH_BATCH_SLOTS)
         k_pool_wait<<<1, 64, 0, c->stream>>>(c->pool_q, (uint32_t)slot, (N + VM_SLICES - 1) / VM_SLICES,
                                              pool_wait_ticks(N), c->pool_err);
@@ -4125,6 +4252,17 @@ int ovh_vm_clock(ovh_ctx* c, uint64_t* stamps, size_t max) {
   const VmDev* d = c->clk_table ? &c->vm_vote_t : &c->vm_vote;
   const size_t n = (size_t)2 * c->clk_wgs, k = max < n ? max : n;
   if (k && hipMemcpy(stamps, d->clk, k * 8, hipMemcpyDeviceToHost) != hipSuccess) return -OVH_ERR_DEVICE;
+  return (int)n;
+}
+
+int ovh_pool_log(ovh_ctx* c, uint64_t* words, size_t max) {
+  if (!c || (max && !words)) return -OVH_ERR_ARG;
+  if (!c->sub.empty()) c = c->sub[0];
+  if (!c->plog) return 0;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (hipSetDevice(c->device) != hipSuccess || sync_all(c)) return -OVH_ERR_DEVICE;
+  const size_t n = PLOG_TOTAL, k = max < n ? max : n;
+  if (k && hipMemcpy(words, c->plog, k * 8, hipMemcpyDeviceToHost) != hipSuccess) return -OVH_ERR_DEVICE;
   return (int)n;
 }
 
@@ -5087,7 +5225,7 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   }
   CHK(ensure_cap(c, n));
   int slot;
-  CHK(take_slot(c, &slot));
+  CHK(pool_take_slot(c, &slot));
   if (!st) {
     CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes));
     CHK(shard_partial(c, slot, (uint32_t)n, d_codes, (uint32_t*)d_partial, nullptr));

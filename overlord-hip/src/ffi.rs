@@ -73,6 +73,7 @@ extern "C" {
     pub fn ovh_vm_trace(ctx: *mut OvhCtx, prog: i32, stamps: *mut u64, max: usize) -> i32;
     pub fn ovh_diag_vm_occupancy(ctx: *mut OvhCtx, prog: i32, n: usize, reps: i32, streams: i32, ms: *mut f32) -> i32;
     pub fn ovh_vm_clock(ctx: *mut OvhCtx, stamps: *mut u64, max: usize) -> i32;
+    pub fn ovh_pool_log(ctx: *mut OvhCtx, words: *mut u64, max: usize) -> i32;
     pub fn ovh_sign_batch_device(ctx: *mut OvhCtx, n: usize, d_sks: *const u8, d_hashes: *const u8, d_sigs: *mut u8) -> i32;
     pub fn ovh_sk_to_pk_batch_device(ctx: *mut OvhCtx, n: usize, d_sks: *const u8, d_pks: *mut u8) -> i32;
 }
