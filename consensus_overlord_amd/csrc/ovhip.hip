@@ -1192,18 +1192,42 @@ __global__ __launch_bounds__(64) void k_vm_g1pairs(uint32_t npairs, VmDev prog, 
   }
 }
 
-// Per distinct hash (one wave): f_g = Miller(apk_g, H_g) -> the group slab's f planes; apk_g =
-// P[head[g]] (its votes' r pk summed, the identity when none of them passed its checks or
-// H_g = O), and then f_g = 1 (e(O, H) = 1).
-__global__ __launch_bounds__(64) void k_vm_gmil(uint32_t G, uint32_t q0, VmDev prog, const uint32_t* __restrict__ cst_g,
-                                                const uint32_t* __restrict__ head, Slab P, Slab g) {
+// The head hash of a same-message batch (one wave): the first hash whose key sum is not the
+// identity (some vote of it passed its checks) and whose H is not O -- its pair joins the final's
+// two-pair loop (k_vm_gfin); 0 when there is none (gfin then finds the batch degenerate). ADVICE
+// r04: with hash 0 always the head, one malformed vote on a fresh hash arriving first made the
+// combined check degenerate and sent every other vote of the batch through the bisection.
+__global__ __launch_bounds__(64) void k_pick_head(uint32_t G, const uint32_t* __restrict__ head, Slab P,
+                                                  const uint32_t* __restrict__ ghinf, uint32_t* __restrict__ sel) {
+  uint32_t best = 0xFFFFFFFFu;
+  for (uint32_t q = threadIdx.x; q < G; q += 64) {
+    Fp z;
+    P.ld(z, 2, head[q]);
+    if (!fp_is_zero(z) && !ghinf[q] && q < best) best = q;
+  }
+  for (uint32_t off = 32; off; off >>= 1) {
+    const uint32_t o = __shfl_xor(best, off);
+    best = o < best ? o : best;
+  }
+  if (threadIdx.x == 0) *sel = best == 0xFFFFFFFFu ? 0u : best;
+}
+
+// Per distinct hash other than the head (one wave each, hashes 0..G-1 with the head skipped):
+// f_g = Miller(apk_g, H_g) -> the group slab's f planes at index g, hash 0's at the head's index
+// (so the fold reads f of indices 1..G-1); apk_g = P[head[g]] (its votes' r pk summed, the
+// identity when none of them passed its checks or H_g = O), and then f_g = 1 (e(O, H) = 1).
+__global__ __launch_bounds__(64) void k_vm_gmil(uint32_t G, const uint32_t* __restrict__ sel, VmDev prog,
+                                                const uint32_t* __restrict__ cst_g, const uint32_t* __restrict__ head,
+                                                Slab P, Slab g) {
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
   uint32_t* slots = lds + SLOT_BASE_W;
   __shared__ uint32_t zinf;
-  const uint32_t q = q0 + blockIdx.x, lane = threadIdx.x;
-  if (q >= G) return;
+  const uint32_t hsel = *sel;
+  const uint32_t q = blockIdx.x, lane = threadIdx.x;
+  if (q >= G || q == hsel) return;
+  const uint32_t oq = q == 0 ? hsel : q;  // the f index this hash's Miller value goes to
   const uint32_t a = head[q];
   load_consts(cst, cst_g, VM_NCONST);
   if (lane == 0) {
@@ -1223,11 +1247,11 @@ __global__ __launch_bounds__(64) void k_vm_gmil(uint32_t G, uint32_t q0, VmDev p
       Fp v;
       if (lane == 0) fp_one(v);
       else fp_zero(v);
-      g.st(v, VM_G_F + lane, q);
+      g.st(v, VM_G_F + lane, oq);
     }
     return;
   }
-  vm::run(prog.code, VM_GMIL_NPHASES, 64, lane, true, slots, cst, 0, vm::Out{g.p, g.cap, q});
+  vm::run(prog.code, VM_GMIL_NPHASES, 64, lane, true, slots, cst, 0, vm::Out{g.p, g.cap, oq});
 }
 
 // The bisection of a same-message batch whose combined check failed (skipped when *verdict == 1):
@@ -1255,22 +1279,22 @@ __global__ __launch_bounds__(64) void k_vm_vote1h_b(uint32_t cnt, uint32_t lo, V
                            ghinf + gid[i]);
 }
 
-// The combined check of a same-message batch (one wave): F (the Miller values of hashes 1..G-1,
-// folded to one; the identity when F.p is null) x Miller(apk_0, H_0) x Miller(-G1, S) as one
-// two-pair Miller loop, then FE == 1 -> *verdict (program gfin). apk_0 = P[head[0]], S = the
-// MSM's sum. When apk_0 or S is the identity (every vote of hash 0 failed, or no vote passed its
-// checks) the pair cannot enter the shared loop: the verdict is 0 and the per-vote bisection
-// decides every code exactly.
+// The combined check of a same-message batch (one wave): F (the Miller values of the other
+// hashes, folded to one; the identity when F.p is null) x Miller(apk_h, H_h) x Miller(-G1, S) as
+// one two-pair Miller loop, then FE == 1 -> *verdict (program gfin). h = *sel (k_pick_head: a
+// hash with a non-identity key sum), apk_h = P[head[h]], S = the MSM's sum. When apk_h or S is
+// the identity (no vote passed its checks) the pair cannot enter the shared loop: the verdict is
+// 0 and the per-vote bisection decides every code exactly.
 static_assert(VM_GFIN_W == 64 && VM_GFIN_NIN == 27, "gfin inputs: F, apk, H, S");
 __global__ __launch_bounds__(64) void k_vm_gfin(VmDev prog, const uint32_t* __restrict__ cst_g, Slab F,
-                                                const uint32_t* __restrict__ head, Slab P, Slab gH, Slab S,
-                                                int32_t* __restrict__ verdict) {
+                                                const uint32_t* __restrict__ head, const uint32_t* __restrict__ sel,
+                                                Slab P, Slab gH, Slab S, int32_t* __restrict__ verdict) {
   extern __shared__ uint4 lds4[];
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
   uint32_t* slots = lds + SLOT_BASE_W;
   __shared__ uint32_t degenerate;
-  const uint32_t lane = threadIdx.x, a = head[0];
+  const uint32_t lane = threadIdx.x, hsel = *sel, a = head[hsel];
   load_consts(cst, cst_g, VM_NCONST);
   if (lane == 0) {
     Fp za, zs;
@@ -1289,7 +1313,7 @@ __global__ __launch_bounds__(64) void k_vm_gfin(VmDev prog, const uint32_t* __re
     } else if (lane < 15) {
       P.ld(v, lane - 12, a);
     } else if (lane < 21) {
-      gH.ld(v, lane - 15, 0);
+      gH.ld(v, lane - 15, hsel);
     } else {
       S.ld(v, lane - 21, 0);
     }
@@ -2826,7 +2850,7 @@ static uint32_t groups_of(uint32_t n) { return (n + GROUP_VOTES - 1) / GROUP_VOT
 // recorded after the publication (pool_join's stream waits for it). alone: the batch's combined
 // check covers only this batch (not a shard of a larger combined check).
 static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
-                       int32_t* d_codes, bool alone = false) {
+                       int32_t* d_codes, bool alone = false, bool launch = true) {
   Slab s{c->state_slot[slot], c->cap};
   c->ev_mask = 0;
   uint64_t seed, base;
@@ -2888,7 +2912,7 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   pa.pt_side = c->vm_vote_t.side;
   pa.fold_code = c->vm_fold.code;
   pa.cst = c->vm_consts;
-  for (uint32_t par = 0; par < 2; ++par) {
+  for (uint32_t par = 0; launch && par < 2; ++par) {
     hipStream_t pst = c->pool_st[par];
     HIPCHK(hipStreamWaitEvent(pst, c->ev_front[slot], 0));
     if (par == 0) {  // the vote stage's and the vote spans' start (stream 0), end (stream 1)
@@ -3384,12 +3408,13 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   if (!c->gslab[slot] || c->gcap[slot] < c->cap) {
     if (c->gslab[slot]) (void)hipFree(c->gslab[slot]);
     c->gslab[slot] = nullptr;
-    HIPCHK(hipMalloc(&c->gslab[slot], ((size_t)VM_G_PLANES * 12 + 1) * c->cap * 4));
+    HIPCHK(hipMalloc(&c->gslab[slot], (((size_t)VM_G_PLANES * 12 + 1) * c->cap + 16) * 4));
     c->gcap[slot] = c->cap;
   }
   const uint32_t G = pl.G, N = (uint32_t)n, T = (uint32_t)t;
   const Slab g{c->gslab[slot], c->gcap[slot]};
   uint32_t* ghinf = c->gslab[slot] + (size_t)VM_G_PLANES * 12 * g.cap;
+  uint32_t* hsel = ghinf + g.cap;  // k_pick_head's choice (the word after the H = O flags)
   const Slab gH{g.p + (size_t)VM_G_H * 12 * g.cap, g.cap};
   const Slab s{c->state_slot[slot], c->cap};
   const Slab P{s.p + (size_t)S_F * 12 * s.cap, s.cap};  // r pk of every vote, then the sums in place
@@ -3467,10 +3492,12 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
       k_vm_g1pairs<<<(np + 64 / VM_G1PADD_W - 1) / (64 / VM_G1PADD_W), 64, LDS_G1PADD, xs>>>(
           np, c->vm_g1padd, G1PADD_STRIDE_W, c->vm_consts, pairs + 2 * (size_t)a, P);
     }
-    // hashes 1..G-1: their own Miller loops, folded to one F; hash 0's pair joins the final's loop
+    // the head hash (k_pick_head) joins the final's loop; the others run their own Miller loops,
+    // folded to one F
+    k_pick_head<<<1, 64, 0, xs>>>(G, head, P, ghinf, hsel);
     if (G > 1) {
       m = (G - 1 + 3) / 4;
-      k_vm_gmil<<<G - 1, 64, LDS_GMIL, xs>>>(G, 1, c->vm_gmil, c->vm_consts, head, P, g);
+      k_vm_gmil<<<G, 64, LDS_GMIL, xs>>>(G, hsel, c->vm_gmil, c->vm_consts, head, P, g);
       k_vm_fold<VM_FOLD_UNITS><<<(m + VM_FOLD_UNITS - 1) / VM_FOLD_UNITS, 64, LDS_FOLD, xs>>>(
           G - 1, c->vm_fold, c->vm_consts, Slab{g.p + (size_t)VM_G_F * 12 * g.cap + 1, g.cap}, Slab{nullptr, 0},
           region_F(c, slot, 0), nullptr);
@@ -3486,7 +3513,7 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   {
     StageScope p(c, ST_FINAL, fst);
     k_vm_gfin<<<1, 64, LDS_GFIN, fst>>>(c->vm_gfin, c->vm_consts, G > 1 ? region_F(c, slot, reg) : Slab{nullptr, 0},
-                                        head, P, gH, msm_S(c, slot), verdict);
+                                        head, hsel, P, gH, msm_S(c, slot), verdict);
   }
   {
     StageScope p(c, ST_FALLBACK, fst);
@@ -4182,7 +4209,8 @@ int ovh_device_count(ovh_ctx* c) { return !c ? 0 : c->sub.empty() ? 1 : (int)c->
 // once the pool finished its previous batch), no final-stream work; `streams` is ignored.
 // *ms = the wall time of the whole sequence (HIP events).
 int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams, float* ms) {
-  if (!c || !ms || n == 0 || n > (1u << 20) || reps < 1 || streams < 1 || streams > 2 || prog < 0 || prog > 1)
+  if (!c || !ms || n == 0 || n > (1u << 20) || reps < 1 || streams < 1 || streams > 2 || prog < 0 || prog > 2 ||
+      (prog == 2 && reps > OVH_BATCH_SLOTS))
     return OVH_ERR_ARG;
   if (!c->sub.empty()) c = c->sub[0];
   std::lock_guard<std::mutex> g(c->mu);
@@ -4208,16 +4236,20 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
                                                                                c->in_buf + n * 128, PkSrc{}, c->in_buf,
                                                                                s, 1, 0, dc);
     } else {
+      // prog 2: every batch published before the pool's grids start (one pair, after the last):
+      // the pool runs without a gap, so under rocprofv3's serialised dispatches (PMC passes) its
+      // counters cover the reps batches and no idle wait for a publication
       const int slot = r % OVH_BATCH_SLOTS;
       k_pool_announce<<<1, 64, 0, c->stream>>>(c->pool_q, c->pool_seq + 1);
       if (r >= OVH_BATCH_SLOTS)
         k_pool_wait<<<1, 64, 0, c->stream>>>(c->pool_q, (uint32_t)slot, (N + VM_SLICES - 1) / VM_SLICES,
                                              pool_wait_ticks(N), c->pool_err);
-      CHK(batch_front(c, slot, N, c->in_buf, c->in_buf + n * 96, KeySrc{c->in_buf + n * 128, PkSrc{}}, dc));
+      CHK(batch_front(c, slot, N, c->in_buf, c->in_buf + n * 96, KeySrc{c->in_buf + n * 128, PkSrc{}}, dc, false,
+                      prog == 1 || r == reps - 1));
     }
   }
   HIPCHK(hipGetLastError());
-  if (prog == 1) c->clk_wgs = c->pool_wgs < VM_CLOCK_WGS ? c->pool_wgs : VM_CLOCK_WGS;
+  if (prog >= 1) c->clk_wgs = c->pool_wgs < VM_CLOCK_WGS ? c->pool_wgs : VM_CLOCK_WGS;
   for (hipStream_t p : {c->xstream, c->pool_st[0], c->pool_st[1]}) {
     HIPCHK(hipEventRecord(e1, p));
     HIPCHK(hipStreamWaitEvent(c->stream, e1, 0));

@@ -266,10 +266,12 @@ int ovh_vote_spans(ovh_ctx* ctx, float* ms, size_t max);
  * read after each phase barrier: copies min(max, nphases + 1) stamps, returns nphases + 1
  * (0 without the flag, <0 on error). */
 int ovh_vm_trace(ovh_ctx* ctx, int prog, uint64_t* stamps, size_t max);
-/* Diagnostics: occupancy A/B of a VM program -- `reps` launches of program `prog` (0 vsame, 1
- * vote) over n votes, on one stream (streams = 1) or alternating over two (streams = 2: two
- * launches co-resident when the LDS allows, i.e. two waves per SIMD); streams = 3: every launch
- * on the pipelined pair's first stream, 4: alternating over the pair. *ms = wall time. */
+/* Diagnostics: `reps` batches of n zero votes through a VM program, *ms = wall time. prog 0:
+ * vsame launches on one stream (streams = 1) or alternating over two (streams = 2: two
+ * launches co-resident when the LDS allows, i.e. two waves per SIMD). prog 1: the vote pool,
+ * batches published back to back (staging, hash_to_field, publication; no final-stream work).
+ * prog 2: the vote pool with all reps <= OVH_BATCH_SLOTS batches published before its grids
+ * start (no gap: the PMC passes' counters cover the batches and no idle wait). */
 int ovh_diag_vm_occupancy(ovh_ctx* ctx, int prog, size_t n, int reps, int streams, float* ms);
 /* Diagnostics (context created with OVH_FLAG_VM_CLOCK): per workgroup of the last vote / vote_t
  * launch, (delta s_memtime, delta s_memrealtime) around its VM program -- shader cycles and

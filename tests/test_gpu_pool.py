@@ -1,0 +1,80 @@
+"""The vote pool (ovhip.hip k_vm_pool; DESIGN.md section 3, "Vote pool") through the pipelined
+C ABI (ovh_verify_batch_device_async + ovh_batch_wait), against the C oracle's per-vote verify.
+
+The pool reads a batch on its own schedule, batches later; the library stages each batch's
+signatures and keys into the batch slot's own buffer on ovh_stream (k_pool_stage) and consumes
+the hashes there (hash_to_field), so the contract of include/ovhip.h holds: the inputs are read
+in ovh_stream order, and work the caller enqueues on ovh_stream after the call may overwrite
+them."""
+import numpy as np
+import pytest
+
+import synth_votes as sv
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def votes():
+    from consensus_overlord_amd.crypto import Context
+    ctx = Context(0)
+    s, h, p = sv.make(ctx, 2048, lo=86000)
+    ctx.close()
+    return s, h, p
+
+
+def test_inputs_overwritten_on_ovh_stream_after_enqueue(votes):
+    """Six pipelined 2,048-vote batches from ONE set of input buffers: after each enqueue the
+    caller overwrites the buffers on ovh_stream -- the next batch's inputs, or junk after the last
+    -- while the pool has not yet reached that batch. Every batch's codes equal the oracle's for
+    the inputs it was enqueued with (batches 1, 3, 5 carry 1% sigma + G2 and a key that does not
+    parse; 0, 2, 4 are valid)."""
+    import torch
+    from consensus_overlord_amd import device as dev
+    from consensus_overlord_amd.crypto import Context
+    s, h, p = votes
+    n = len(s)
+    bad_s, bad_p = s.copy(), p.copy()
+    flagged = sv.seeded_positions(n, 0.01, 51)
+    for i in flagged:
+        bad_s[i] = np.frombuffer(sv.add_g2(bytes(bad_s[i])), dtype=np.uint8)
+    bad_p[7] = np.frombuffer(bytes.fromhex("ff" * 48), dtype=np.uint8)
+    jobs = [(s, p) if k % 2 == 0 else (bad_s, bad_p) for k in range(6)]
+    want_bad = sv.oracle_codes(bad_s, h, bad_p)
+    assert (want_bad != 0).sum() == len(flagged) + (0 if 7 in flagged else 1)
+
+    ctx = Context(0)
+    ovh = torch.cuda.ExternalStream(ctx.stream)
+    d_s = torch.empty((n, 96), dtype=torch.uint8, device="cuda")
+    d_h = torch.from_numpy(h).cuda()
+    d_p = torch.empty((n, 48), dtype=torch.uint8, device="cuda")
+    # the batches' inputs as device tensors made on torch's stream before the loop (device-to-device
+    # copies on ovh_stream below: no pinned host block records an event on the library's stream)
+    src = [(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()) for a, b in jobs]
+    codes = [torch.full((n,), -1, dtype=torch.int32, device="cuda") for _ in jobs]
+    junk = torch.full((n, 96), 0xFF, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    with torch.cuda.stream(ovh):
+        d_s.copy_(src[0][0])
+        d_p.copy_(src[0][1])
+    for k in range(len(jobs)):
+        dev.verify_batch_async(ctx, d_s, d_h, d_p, codes[k])
+        with torch.cuda.stream(ovh):   # stream-ordered after the call: the library has staged them
+            if k + 1 < len(jobs):
+                d_s.copy_(src[k + 1][0])
+                d_p.copy_(src[k + 1][1])
+            else:
+                d_s.copy_(junk)
+                d_p.copy_(junk[:, :48])
+                d_h.zero_()
+    dev.batch_wait(ctx)
+    torch.cuda.synchronize()
+    for k in range(len(jobs)):
+        got = codes[k].cpu().numpy()
+        if k % 2 == 0:
+            assert (got == 0).all(), (k, np.nonzero(got)[0][:8])
+        else:
+            assert got.tolist() == want_bad.tolist(), k
+    del src, d_s, d_h, d_p, junk, codes
+    torch.cuda.synchronize()
+    ctx.close()

@@ -200,3 +200,40 @@ def test_device_async_pipeline_codes_equal_oracle():
         want = sv.oracle_codes(s, np.tile(np.frombuffer(d, dtype=np.uint8), (len(s), 1)), p)
         assert c.cpu().numpy().tolist() == want.tolist()
     assert codes[1].cpu().numpy()[[7, 150, 299]].tolist() != [0, 0, 0]
+
+
+def test_first_hash_all_malformed_takes_no_bisection():
+    """a fresh hash whose only votes are malformed (96 bytes that do not
+    parse), arriving first, must not make the combined check degenerate. Its key sum is the
+    identity, so the device picks the next hash as the head of the final's two-pair loop
+    (k_pick_head): the codes equal the oracle's and the batch's bisection stage does no per-vote
+    work (stage time, OVH_FLAG_PROFILE context) -- with hash 0 as the fixed head every valid vote
+    went through a per-vote Miller loop and final exponentiation."""
+    import ctypes
+    import consensus_overlord_amd as coa
+    from consensus_overlord_amd.crypto import Context, FLAG_PROFILE
+    os.environ["OVH_SAMEMSG"] = "2"
+    try:
+        ctx = Context(0, flags=FLAG_PROFILE)
+    finally:
+        del os.environ["OVH_SAMEMSG"]
+    cc = coa.ConsensusCrypto(bytes.fromhex("71" * 32), ctx=ctx)
+    da, db = sv.sha(b"fresh hash, malformed votes"), sv.sha(b"round 12 precommit")
+    sb, pb = _round(cc.ctx, 85000, 48, db)
+    junk = np.frombuffer(bytes.fromhex("ff" * 96), dtype=np.uint8)
+    sa, pa = np.stack([junk] * 3), pb[:3].copy()
+    sigs, pks = np.concatenate([sa, sb]), np.concatenate([pa, pb])
+    hs = np.concatenate([np.tile(np.frombuffer(da, dtype=np.uint8), (3, 1)),
+                         np.tile(np.frombuffer(db, dtype=np.uint8), (48, 1))])
+    want = sv.oracle_codes(sigs, hs, pks)
+    assert want[:3].tolist() == [1, 1, 1] and want[3:].tolist() == [0] * 48
+    b0 = cc.samemsg_stats()
+    got = cc.verify_batch(list(map(bytes, sigs)), list(map(bytes, hs)), list(map(bytes, pks)))
+    assert got.tolist() == want.tolist()
+    assert cc.samemsg_stats()[0] == b0[0] + 1
+    names = [ctx.lib.ovh_stage_name(k).decode() for k in range(6)]
+    ms = (ctypes.c_float * 6)()
+    assert ctx.lib.ovh_stage_times(ctx.ptr, ms, 6) == 6
+    # the per-vote bisection of 48 votes is milliseconds of Miller loops and final
+    # exponentiations; skipped, its kernels exit at their first instruction
+    assert ms[names.index("bisect")] < 0.5, list(ms)

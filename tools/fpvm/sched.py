@@ -501,6 +501,10 @@ def encode(sc):
         sw = [0] * sc.W
         for k, i in enumerate(sides):
             v = i if ops[i].kind == "fill" else ops[i].srcs[0]
+            # the fields' widths (fpvm.hpp side_spill / run masks 0x7FF, 0xFFF): a wider slot or
+            # scratch entry would alias another one on the device
+            assert sc.slot_of[v] < 1 << 11, ("side word slot", sc.slot_of[v])
+            assert 0 <= ops[i].imm < 1 << 12, ("side word scratch entry", ops[i].imm)
             sw[k] = 1 << 31 | (ops[i].kind == "fill") << 30 | sc.slot_of[v] | ops[i].imm << 11
             assert sc.slot_of[v] < 2048 and ops[i].imm < 4096
         sc.side_words += sw
