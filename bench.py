@@ -478,6 +478,9 @@ def main():
     ap.add_argument("--clock-seconds", type=float, default=2.0,
                     help="diagnostic pass after the timed region: back-to-back batches on a context with "
                          "OVH_FLAG_VM_CLOCK for this long, then the vote kernel's held clock (0 = skip)")
+    ap.add_argument("--plain-timed-ctx", action="store_true",
+                    help="A/B: time the batches on a context without OVH_FLAG_PROFILE (no HIP events in the timed "
+                         "region; vote_spans then absent and the roofline uses the profile batches' stage time)")
     ap.add_argument("--shard-path", action="store_true",
                     help="diagnostic: run the multi-GPU pipeline (partials + RCCL all-gather) even at N=1")
     ap.add_argument("--multi-device", default=None, metavar="DEVS",
@@ -520,6 +523,9 @@ def main():
     nbatch = args.warmup + args.steps + args.profile_steps
     codes = torch.full((nbatch, B), -1, dtype=torch.int32, device="cuda")   # one verdict row per batch
     shards = ShardVerifier(DeviceBackend(ctx)) if (world > 1 or args.shard_path) else None
+    # the timed batches' context: the profiling one (HIP events around each batch's pool grids
+    # and stages: vote_spans) unless --plain-timed-ctx
+    tctx = ctx if (shards is not None or not args.plain_timed_ctx) else Context(local, flags=0)
     torch.cuda.synchronize()
 
     nst = NSTAGES
@@ -531,14 +537,14 @@ def main():
         if shards:
             shards.wait()
         else:
-            dev.batch_wait(ctx)
+            dev.batch_wait(tctx)
 
-    def step(s: int) -> None:
+    def step(s: int, c=None) -> None:
         """Enqueue batch s. Pipelined: batch s's combined check / bisection (second stream)
         overlaps batch s + 1's per-vote stages; every batch's codes row is final after
         batch_wait. Each batch's RLC coefficients come from a fresh getrandom seed (library)."""
         if shards is None:
-            dev.verify_batch_async(ctx, sigs, hs, pks, codes[s])
+            dev.verify_batch_async(c or tctx, sigs, hs, pks, codes[s])
         else:
             shards.submit(s, sigs, hs, pks, codes[s], index_base=rank * B)
 
@@ -549,7 +555,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    lib.ovh_vote_spans(ctx.ptr, None, 0)    # forget the warmup batches' vote kernel events
+    lib.ovh_vote_spans(tctx.ptr, None, 0)   # forget the warmup batches' vote kernel events
     t0 = time.perf_counter()
     for s in range(args.steps):
         step(args.warmup + s)
@@ -564,7 +570,7 @@ def main():
     # run two at a time on the per-vote stream pair, so the kernel's device-level time per batch
     # is the union of the spans over the batches, and the mean span is one launch's duration
     sp = (ctypes.c_float * (2 * args.steps))()
-    nsp = lib.ovh_vote_spans(ctx.ptr, sp, 2 * args.steps)
+    nsp = lib.ovh_vote_spans(tctx.ptr, sp, 2 * args.steps)
     vote_spans = None
     if nsp == args.steps and nsp > 0:
         iv = sorted((sp[2 * k], sp[2 * k + 1]) for k in range(nsp))
@@ -590,8 +596,11 @@ def main():
     for s in range(args.warmup + args.steps, nbatch):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        step(s)
-        wait_all()
+        step(s, ctx)
+        if shards is None:
+            dev.batch_wait(ctx)
+        else:
+            wait_all()
         lat.append(time.perf_counter() - t1)
         got = lib.ovh_stage_times(ctx.ptr, buf, nst)
         if got != nst:
@@ -614,15 +623,15 @@ def main():
         dom = max((k for k in range(nst) if names[k] in STAGE_TO_WORK), key=lambda k: avg_ms[k])
         dname = names[dom]
         units = 1 if dname in PER_BATCH_STAGES else B
-        # HBM bytes per launch of the dominant kernel from the committed PMC pass
-        # (tools/pmc_round.sh; FETCH_SIZE doubled per the gfx950 correction); null if absent
-        traffic = None
-        tpath = os.path.join(ROOT, "consensus_overlord_amd", "pmc_traffic.json")
-        if os.path.exists(tpath):
-            with open(tpath) as fh:
-                tk = json.load(fh)["kernels"].get("k_vm_" + dname)
-            if tk is not None and B == 4096:
-                traffic = tk["hbm_bytes_per_launch"]
+        # the vote pool's committed PMC passes (tools/pmc_pool.sh -> tools/pmc_pool_summary.py):
+        # HBM bytes per 4,096-vote batch (FETCH_SIZE doubled per the gfx950 correction) and the
+        # instruction counts per quad for the counter decomposition below; null if absent
+        pmc = None
+        ppath = os.path.join(ROOT, "consensus_overlord_amd", "pmc_pool.json")
+        if os.path.exists(ppath):
+            with open(ppath) as fh:
+                pmc = json.load(fh)
+        traffic = pmc["hbm_bytes_per_batch"] if (pmc and dname == "vote" and B == 4096) else None
         # algorithmic work of the dominant stage: SURVEY.md 8(d) canonical W_v = 18,300 M per vote
         # (Appendix C) less the Pippenger MSM share (350 M), the Fp12 merge (54 M) and the
         # amortised final exponentiation (4 M), which other kernels do; the program's own count
@@ -630,14 +639,41 @@ def main():
         canon = {"vote": W_V_CANON - W_MSM - 54 - 4}
         work_M = canon.get(dname, Mu[STAGE_TO_WORK[dname]])
         macs = work_M * units * macs_per_M
-        # the vote kernel's time per batch: device-level over the timed region (vote_spans) when
-        # recorded, else the unpipelined profile batches' HIP-event stage time
+        # the vote pool's device time per batch over the timed region (vote_spans: the union of
+        # the pool streams' HIP-event spans / batches) when recorded, else the unpipelined profile
+        # batches' HIP-event stage time
         kern_ms = vote_spans["device_ms_per_launch"] if (dname == "vote" and vote_spans) else avg_ms[dom]
         achieved = macs / (kern_ms * 1e-3) / 1e12
         prog_achieved = Mu[STAGE_TO_WORK[dname]] * units * macs_per_M / (kern_ms * 1e-3) / 1e12
         value = world * B * args.steps / elapsed
         path_M = W_V_CANON
         held = clock["clock_ghz"] if clock else None
+        # counter decomposition of frac: frac = VALU busy x v_mad share x
+        # useful MACs per issued v_mad lane-op x (4.14 / 4 cycles per v_mad at the peak's rate) x
+        # (clock / the peak's clock); VALU busy from the PMC instruction count per quad and this
+        # run's time per batch, 1,024 SIMDs at the held clock (2.371 GHz without the clock pass)
+        decomp = None
+        if pmc and dname == "vote" and B == 4096 and pmc.get("valu_per_quad"):
+            ghz = held or PEAK_MAD_U64_CLOCK_GHZ
+            quads = B // 4
+            busy = quads * pmc["valu_per_quad"] * 4 / (1024 * ghz * 1e9 * kern_ms * 1e-3)
+            mad_share = pmc["mad_per_quad_static"] / pmc["valu_per_quad"]
+            lane_use = 4 * work_M * macs_per_M / (pmc["mad_per_quad_static"] * 64)
+            issue = 4.14 / 4 * ghz / PEAK_MAD_U64_CLOCK_GHZ
+            pred = busy * mad_share * lane_use * issue
+            decomp = {"valu_busy": round(busy, 4), "mad_share": round(mad_share, 4), "lane_use": round(lane_use, 4),
+                      "issue_factor": round(issue, 4), "product": round(pred, 4),
+                      "product_over_frac": round(pred / (achieved * 1e12 / PEAK_MAD_U64), 4),
+                      "valu_per_quad": pmc["valu_per_quad"], "mad_per_quad": pmc["mad_per_quad_static"],
+                      "lanes_per_valu": pmc.get("lanes_per_valu"),
+                      "wait_any_share": pmc.get("wait_any_share"), "wait_basis": pmc.get("wait_basis"),
+                      "lds_bank_conflict_share": pmc.get("lds_bank_conflict_share"),
+                      "write_kb_per_batch": pmc.get("write_kb_per_batch"),
+                      "basis": "valu_busy = 1,024 quads x SQ_INSTS_VALU per quad x 4 cycles / (1,024 SIMDs x clock x "
+                               "kernel_ms_per_batch); mad_share = static v_mad_u64_u32 per quad / SQ_INSTS_VALU per "
+                               "quad; lane_use = algorithmic MACs per quad / (v_mad per quad x 64 lanes); "
+                               "issue_factor = 4.14 / 4 x clock / 2.371 GHz (the peak's measured v_mad rate); "
+                               "counters: " + pmc["source"]}
         line = {
             "metric": "BLS12-381 vote verifications/sec (batch 4096) at 1/2/4/8 MI355X vs host blst",
             "value": round(value, 2),
@@ -660,9 +696,11 @@ def main():
                 "kernel": dname,
                 "achieved": round(achieved, 3),
                 "kernel_ms_per_batch": round(float(kern_ms), 4),
-                "time_basis": ("union of the timed vote kernels' HIP-event spans / launches (two batches' grids "
-                               "co-resident on the per-vote stream pair; launch_ms = one launch's mean span, what "
-                               "rocprof averages)" if (dname == "vote" and vote_spans)
+                "time_basis": ("the vote pool's device time per batch: union over the timed batches of the HIP-event "
+                               "spans around each batch's pool grids on the two pool streams, / batches (the grids "
+                               "are persistent: a batch's span runs from its grids' launch point on the pool streams "
+                               "to their exit, and consecutive spans overlap; launch_ms = the mean span)"
+                               if (dname == "vote" and vote_spans)
                                else "HIP-event stage time of the unpipelined profile batches"),
                 "vote_spans": vote_spans,
                 "peak": round(PEAK_MAD_U64 / 1e12, 3),
@@ -687,7 +725,9 @@ def main():
                 "program_M_per_unit": Mu[STAGE_TO_WORK[dname]],
                 "program_frac": round(prog_achieved * 1e12 / PEAK_MAD_U64, 4),
                 "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x 2 + WRITE_SIZE, pmc_traffic.json)",
+                "traffic_unit": "HBM bytes per 4,096-vote batch of the vote pool (PMC FETCH_SIZE x 2 + WRITE_SIZE, "
+                                "consensus_overlord_amd/pmc_pool.json)",
+                "pmc": decomp,
                 "msm": ({"ms": round(float(avg_ms[names.index("msm")]), 4), "work_M_per_unit": W_MSM,
                          "frac": round(W_MSM * B * macs_per_M / (avg_ms[names.index("msm")] * 1e-3) / PEAK_MAD_U64, 4)}
                         if avg_ms[names.index("msm")] > 0 else None),
@@ -697,14 +737,18 @@ def main():
             "stage_ms": stages,
             "batch_latency_ms": round(float(np.median(lat)) * 1e3, 3) if lat else None,
             "enqueue_ms_per_step": round(enqueue_s / args.steps * 1e3, 4),
-            "pipelined": "batch k's combined check + bisection (second stream) overlap batch k+1's per-vote "
-                         "stages; all %d timed batches complete inside the timed region" % args.steps,
+            "pipelined": "the vote pool runs every batch's per-vote work (persistent grids, quads claimed across "
+                         "batches); batch k's fold, MSM, combined check and bisection run on one of three final "
+                         "streams beside later batches' votes; all %d timed batches complete inside the timed "
+                         "region" % args.steps,
         }
         if world == 1 and not args.no_latency:
             line["latency"] = latencies(ctx, sigs, hs, pks)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(sigs.cpu().numpy(), hs_h, pks.cpu().numpy(), args.cpu_seconds)
         print(json.dumps(line), flush=True)
+    if tctx is not ctx:
+        tctx.close()
     ctx.close()
     if dist.is_initialized():
         dist.destroy_process_group()
