@@ -209,11 +209,15 @@ int ovh_combine_partials_device(ovh_ctx* ctx, size_t k, const uint8_t* d_partial
 int ovh_batch_fallback_device(ovh_ctx* ctx, size_t n, int32_t* d_codes);
 
 /* Pipelined batches. ovh_verify_batch_device_async enqueues one batch and returns without
- * waiting: the per-vote stages run on ovh_stream, the combined check and (device-gated)
- * bisection on a second, lower-priority stream, so batch k's final exponentiation overlaps batch
- * k + 1's per-vote work. Up to OVH_BATCH_SLOTS batches may be in flight per context; the
- * d_codes of a batch must stay untouched until ovh_batch_wait returns, after which they hold
- * exactly the per-vote ovh_verify results. */
+ * waiting: the batch is staged and published on ovh_stream (its signatures and keys copied into
+ * the library's own buffer, its hashes through hash_to_field), its per-vote work runs in the
+ * context's vote pool (persistent workgroups that take 4-vote quads of the published batches in
+ * order), and its combined check and (device-gated) bisection on a lower-priority final stream,
+ * so batch k's final exponentiation overlaps later batches' per-vote work. The inputs are read
+ * in ovh_stream order: they must be ready when the work enqueued there before the call is done,
+ * and work enqueued there after the call may overwrite them. Up to OVH_BATCH_SLOTS batches may be
+ * in flight per context; the d_codes of a batch must stay untouched until ovh_batch_wait
+ * returns, after which they hold exactly the per-vote ovh_verify results. */
 #define OVH_BATCH_SLOTS 6 /* batches in flight per context (state slots) */
 int ovh_verify_batch_device_async(ovh_ctx* ctx, size_t n, const uint8_t* d_sigs, const uint8_t* d_hashes,
                                   const uint8_t* d_pks, int32_t* d_codes);
