@@ -1043,12 +1043,26 @@ static_assert(VM_VSAME_W == 16 && VM_VSAME_T_W == 16 && VM_H2G_W == 16 && VM_GMI
 // Per vote (16-lane slice, 4 per workgroup): votes lo + j, j < cnt (key bytes at pks + 48 j, or
 // table entry pk.idx[j]; signature at sigs + 96 j); stores sigma, tau and r pk at slab index
 // lo + j; code in the reference precedence without the H = O case (k_samemsg_fix adds it).
+// Same-message pipeline (r05ag/r05ah, tools/samemsg_pipe.py, 24 batches of 4,096 votes, ms per
+// batch): the per-vote vsame waves at the pool's priority (2), hash_to_G2 and gfin above them (3):
+// 2.54 -> 2.43; the one-hash API's hash_to_G2 on SM_H2G_STREAMS streams in turn instead of one:
+// 2 streams 2.06-2.08, 3 streams 1.99-2.00, 4 2.03-2.12. (r05aj: vsame in the vote pool ran 4.9
+// ms per batch -- hash_to_G2 (24 KB of LDS) and gfin (34 KB) do not fit the pool's one place per
+// CU and waited for the pool to drain; reverted)
+#ifndef SM_PRIO
+#define SM_PRIO 1
+#endif
+#ifndef SM_H2G_STREAMS
+#define SM_H2G_STREAMS 3
+#endif
+static_assert(SM_H2G_STREAMS >= 1 && SM_H2G_STREAMS <= 4, "hstream[4]");
 template <bool TABLE>
 __global__ __launch_bounds__(64) void k_vm_vsame(uint32_t cnt, uint32_t lo, VmDev prog,
                                                  const uint32_t* __restrict__ cst_g, const uint8_t* __restrict__ pks,
                                                  PkSrc pk, const uint8_t* __restrict__ sigs, Slab s, uint64_t seed,
                                                  uint64_t base, int32_t* __restrict__ codes) {
   extern __shared__ uint4 lds4[];
+  if (SM_PRIO) __builtin_amdgcn_s_setprio(2);
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
   const uint32_t slice = threadIdx.x / 16, lane = threadIdx.x % 16;
@@ -1119,6 +1133,7 @@ __global__ __launch_bounds__(64) void k_vm_vsame(uint32_t cnt, uint32_t lo, VmDe
 __global__ __launch_bounds__(64) void k_vm_h2g(uint32_t G, VmDev prog, const uint32_t* __restrict__ cst_g, Slab g,
                                                uint32_t* __restrict__ ghinf) {
   extern __shared__ uint4 lds4[];
+  if (SM_PRIO) __builtin_amdgcn_s_setprio(3);
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
   const uint32_t slice = threadIdx.x / 16, lane = threadIdx.x % 16;
@@ -1290,6 +1305,7 @@ __global__ __launch_bounds__(64) void k_vm_gfin(VmDev prog, const uint32_t* __re
                                                 const uint32_t* __restrict__ head, const uint32_t* __restrict__ sel,
                                                 Slab P, Slab gH, Slab S, int32_t* __restrict__ verdict) {
   extern __shared__ uint4 lds4[];
+  if (SM_PRIO) __builtin_amdgcn_s_setprio(3);
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
   uint32_t* slots = lds + SLOT_BASE_W;
@@ -2290,6 +2306,7 @@ struct ovh_ctx {
   hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse; lazy)
   // ovh_verify_samemsg_device_async: [0], [1] the per-vote streams, in turn; [2] hash_to_G2 (lazy)
   hipStream_t vstream[3] = {};
+  hipStream_t hstream[4] = {};  // the one-hash API's hash_to_G2 streams in turn ([0] unused: xstream; lazy)
   // the vote pool (k_vm_pool): its two streams (created with the context, high priority), the
   // device queue (PQ_WORDS words), the published batches' descriptors (one per slot), the
   // workgroups' spill scratch (2 x pool_wgs x 4 x VOTE_NSCR entries: one area per pool stream),
@@ -2672,7 +2689,8 @@ static int sync_all(ovh_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->fstream));
   HIPCHK(hipStreamSynchronize(c->fstream2));
   HIPCHK(hipStreamSynchronize(c->fstream3));
-  for (hipStream_t s : {c->pool_st[0], c->pool_st[1], c->vstream[0], c->vstream[1], c->vstream[2]})
+  for (hipStream_t s : {c->pool_st[0], c->pool_st[1], c->vstream[0], c->vstream[1], c->vstream[2], c->hstream[1],
+                        c->hstream[2], c->hstream[3]})
     if (s) HIPCHK(hipStreamSynchronize(s));
   if (c->pool_err && __atomic_load_n(c->pool_err, __ATOMIC_ACQUIRE)) return OVH_ERR_DEVICE;
   return 0;
@@ -3451,7 +3469,11 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   // per-vote work (r04n), so the one-hash path runs on three high-priority streams (a pool of
   // their own: the two per-vote streams and this one) and the final streams (its key sums there).
   if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
-  const hipStream_t xs = one ? fst : c->xstream, hs = c->xstream;
+  // hash_to_G2 of the one-hash API: SM_H2G_STREAMS streams in turn (one wave each; on a single
+  // stream consecutive batches' hash_to_G2 ran back to back)
+  const uint32_t hk = one ? (uint32_t)(c->pipe_k % SM_H2G_STREAMS) : 0u;
+  if (hk && !c->hstream[hk]) HIPCHK(hipStreamCreateWithFlags(&c->hstream[hk], hipStreamNonBlocking));
+  const hipStream_t xs = one ? fst : c->xstream, hs = hk ? c->hstream[hk] : c->xstream;
   HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));  // the inputs (and the slot free: take_slot)
   HIPCHK(hipStreamWaitEvent(hs, c->ev_front[slot], 0));
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
@@ -4150,7 +4172,7 @@ static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
-                        c->pool_st[1]})
+                        c->pool_st[1], c->hstream[1], c->hstream[2], c->hstream[3]})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->grp_ok[k], (void*)c->msm_buf[k], (void*)c->gslab[k]})
@@ -4186,7 +4208,7 @@ static void destroy_one(ovh_ctx* c) {
   }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
-                        c->pool_st[1]})
+                        c->pool_st[1], c->hstream[1], c->hstream[2], c->hstream[3]})
     if (s) (void)hipStreamDestroy(s);
   if (c->pool_err) (void)hipHostFree(c->pool_err);
   delete c;

@@ -7,7 +7,8 @@
 #   SMOKE=1   __graft_entry__.smoke()
 #   BENCH=1   bench.py --steps $STEPS (BENCH_ARGS appended)
 #   PROF=1    rocprofv3 --kernel-trace --stats over a short bench
-#   PMC=1     tools/pmc_round.sh (counter passes, one run each)
+#   PMC=1     tools/pmc_pool.sh (the vote pool's counter passes, one run each; then
+#             python tools/pmc_pool_summary.py $TAG on the CPU side)
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
@@ -34,6 +35,6 @@ if [ -n "${PROF:-}" ]; then
   cd "$R"
 fi
 if [ -n "${PMC:-}" ]; then
-  OUTDIR="$OUT" bash tools/pmc_round.sh > "$OUT/pmc.log" 2>&1
+  TAG=${TAG:-run} bash tools/pmc_pool.sh > "$OUT/pmc.log" 2>&1
 fi
 echo done > "$OUT/ok"
