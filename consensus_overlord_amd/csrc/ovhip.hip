@@ -459,6 +459,8 @@ struct PoolArgs {
   const uint32_t* cst;
   uint32_t* scr;  // VM_SLICES x VOTE_NSCR entries per workgroup
   uint64_t* wlog;  // OVH_FLAG_VM_CLOCK: this grid's workgroup log (PLOG_WG_WORDS per workgroup), else null
+  uint64_t only;   // ~0: claim any batch; else this grid's own batch: its workgroups leave once
+                   // `cur` has passed it (the shard path's grid per batch, ovh_batch_partial_device)
 };
 
 __device__ __forceinline__ uint64_t* pq_done(uint64_t* q, uint32_t slot) { return q + PQ_DONE + slot * POOL_QW; }
@@ -522,12 +524,16 @@ __device__ __forceinline__ uint64_t qldu(const uint64_t* p) {
   return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 __device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* slot_out, uint32_t* quad_out,
-                               uint32_t* why) {
+                               uint32_t* why, uint64_t only) {
   uint64_t t0 = wclock();
   *why = 3;
 #pragma unroll 1
   for (uint32_t tries = 0; tries < (1u << 22); ++tries) {
     const uint64_t s = qldu(q + PQ_CUR), np = qldu(q + PQ_NPUB);
+    if (s > only) {  // a grid of one batch: that batch is fully claimed
+      *why = 4;
+      return 0;
+    }
     if (s >= np) {
       const uint64_t idle = wclock() - t0;
       if (idle > POOL_WAIT_TICKS ||
@@ -758,7 +764,7 @@ __global__ __launch_bounds__(64, 2) void k_vm_pool(PoolArgs a) {
 #pragma unroll 1
   for (;; ++nquads) {
     uint32_t slot = 0, quad = 0;
-    if (!pool_claim(a.q, a.descs, &slot, &quad, &why)) break;
+    if (!pool_claim(a.q, a.descs, &slot, &quad, &why, a.only)) break;
     slot = uni(slot);
     quad = uni(quad);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this batch's descriptor and inputs, fresh
@@ -2507,10 +2513,8 @@ static_assert(VOTE_NSCR <= 4096 && VM_VOTE_NSLOTS <= 2048 && VM_VOTE_T_NSLOTS <=
 #ifndef POOL_HOLES_PER_8CU
 #define POOL_HOLES_PER_8CU 8u
 #endif
-// or: CUs kept from the pool streams (CU mask), the pool filling the others (8 per CU)
-#ifndef POOL_RESERVE_CUS
-#define POOL_RESERVE_CUS 0u
-#endif
+// (r05s: CU-masked pool streams -- the pool on 8 places of 240 or 224 CUs, the rest for the side
+// kernels -- ran 1.02M / 0.96M verifs/s against 1.42M; removed)
 #define POOL_MAX_WGS 4096u
 static_assert(FOLD_STRIDE_W <= VM_SLICES * VOTE_STRIDE_W && FOLD_STRIDE_W <= VM_SLICES * VOTE_T_STRIDE_W,
               "fused fold reuses the vote slots");
@@ -2868,7 +2872,7 @@ static uint32_t groups_of(uint32_t n) { return (n + GROUP_VOTES - 1) / GROUP_VOT
 // recorded after the publication (pool_join's stream waits for it). alone: the batch's combined
 // check covers only this batch (not a shard of a larger combined check).
 static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, const uint8_t* d_hashes, KeySrc key,
-                       int32_t* d_codes, bool alone = false, bool launch = true) {
+                       int32_t* d_codes, bool alone = false, bool launch = true, bool shard = false) {
   Slab s{c->state_slot[slot], c->cap};
   c->ev_mask = 0;
   uint64_t seed, base;
@@ -2921,7 +2925,9 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   // refills from the next batch's grids, and a batch alone still gets every place
   const bool vev = (c->flags & OVH_FLAG_PROFILE) != 0;
   const uint32_t vk = c->vev_n % ovh_ctx::VEV_CAP;
+  const uint32_t wgs = c->pool_wgs;
   PoolArgs pa;
+  pa.only = ~0ull;
   pa.q = c->pool_q;
   pa.descs = (const PoolBatch*)c->pool_desc;
   pa.pv_code = c->vm_vote.code;
@@ -2931,21 +2937,28 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   pa.fold_code = c->vm_fold.code;
   pa.cst = c->vm_consts;
   for (uint32_t par = 0; launch && par < 2; ++par) {
+    // the shard path: one grid of this batch alone per batch, on the pool streams in turn (its
+    // workgroups leave when the batch is claimed, so the caller's collective finds places between
+    // batches -- with persistent grids it waited for the pool to drain, r05an / r05aq pool logs)
+    if (shard && par != (uint32_t)(seq & 1)) continue;
+    if (shard) pa.only = seq;
     hipStream_t pst = c->pool_st[par];
     HIPCHK(hipStreamWaitEvent(pst, c->ev_front[slot], 0));
-    if (par == 0) {  // the vote stage's and the vote spans' start (stream 0), end (stream 1)
+    if (par == 0 || shard) {  // the vote stage's and the vote spans' start (stream 0), end (stream 1)
       if (c->flags & OVH_FLAG_PROFILE) HIPCHK(hipEventRecord(c->ev0[ST_VOTE], pst));
       if (vev) HIPCHK(hipEventRecord(c->vev0[vk], pst));
     }
-    pa.scr = c->pool_scr + (size_t)par * c->pool_wgs * VM_SLICES * VOTE_NSCR * 12;
+    // each workgroup's own scratch: grid par's workgroups at par x (its size): the two streams'
+    // grids may be co-resident (a shard grid is twice the size)
+    pa.scr = c->pool_scr + (size_t)par * (shard ? 2 : 1) * c->pool_wgs * VM_SLICES * VOTE_NSCR * 12;
     pa.wlog = nullptr;
     if (c->plog) {  // grid record: [seq, par, workgroups, -], then the workgroups'
       uint64_t* g = c->plog + PLOG_GRID_BASE + (size_t)(c->plog_grids++ % PLOG_GRIDS) * (4 + PLOG_WGS * PLOG_WG_WORDS);
-      k_grid_hdr<<<1, 64, 0, pst>>>(g, seq, par, c->pool_wgs);
+      k_grid_hdr<<<1, 64, 0, pst>>>(g, seq, par, shard ? 2 * wgs : wgs);
       pa.wlog = g + 4;
     }
-    k_vm_pool<<<c->pool_wgs, 64, LDS_POOL, pst>>>(pa);
-    if (par == 1) {
+    k_vm_pool<<<shard ? 2 * wgs : wgs, 64, LDS_POOL, pst>>>(pa);
+    if (par == 1 || shard) {
       if (c->flags & OVH_FLAG_PROFILE) {
         HIPCHK(hipEventRecord(c->ev1[ST_VOTE], pst));
         c->ev_mask |= 1u << ST_VOTE;
@@ -3679,7 +3692,7 @@ static int verify_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
       CHK(pool_take_slot(s, &p.slot));
       s->test_base = root->test_base + lo + plo;  // OVH_FLAG_TEST_RLC only: one global index per vote
       CHK(batch_front(s, p.slot, (uint32_t)pc, in + 96 * plo, in + cnt * 96 + 32 * plo, staged_key(s, cnt, in, t, plo),
-                      dcodes[d] + plo));
+                      dcodes[d] + plo, false, true, true));
       uint32_t* po = s->part_out + (size_t)(parts[d].size()) * (OVH_PARTIAL_BYTES / 4);
       CHK(shard_partial(s, p.slot, (uint32_t)pc, dcodes[d] + plo, po, nullptr));
       // partial -> devices[0] (peer copy over xGMI), ordered on this device's stream
@@ -3905,7 +3918,7 @@ static int submit_host_multi(ovh_ctx* root, size_t n, const uint8_t* sigs, const
       CHK(pool_take_slot(s, &slot));
       s->test_base = root->test_base + lo + plo;  // OVH_FLAG_TEST_RLC only: one global index per vote
       CHK(batch_front(s, slot, (uint32_t)pc, in + 96 * plo, in + cnt * 96 + 32 * plo, staged_key(s, cnt, in, t, plo),
-                      dcodes + plo));
+                      dcodes + plo, false, true, true));  // (peer copies of the partials: grids per batch)
       const hipStream_t fst = s->fs[slot];
       int reg;
       uint32_t m;
@@ -4036,19 +4049,6 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   // pool's places are split between the grids of the two pool streams (batch_front), which run
   // side by side: each grid holds half of them
   c->pool_wgs = ((uint32_t)ncu * 8 - (uint32_t)ncu * POOL_HOLES_PER_8CU / 8) / 2;
-  std::vector<uint32_t> pool_mask;
-  if (POOL_RESERVE_CUS > 0 && (uint32_t)ncu >= 8 * POOL_RESERVE_CUS) {
-    // reserved CU k: bit s k + k % 8 (s = ncu / reserve), so the reserved CUs spread over the
-    // XCDs whether the mask's bits run XCD by XCD or round-robin over them
-    const uint32_t st = (uint32_t)ncu / POOL_RESERVE_CUS;
-    pool_mask.assign(((uint32_t)ncu + 31) / 32, 0u);
-    for (uint32_t i = 0; i < (uint32_t)ncu; ++i) pool_mask[i / 32] |= 1u << (i % 32);
-    for (uint32_t k = 0; k < POOL_RESERVE_CUS; ++k) {
-      const uint32_t b = st * k + k % 8;
-      pool_mask[b / 32] &= ~(1u << (b % 32));
-    }
-    c->pool_wgs = ((uint32_t)ncu - POOL_RESERVE_CUS) * 8 / 2;
-  }
   if (c->pool_wgs > POOL_MAX_WGS) c->pool_wgs = POOL_MAX_WGS;
   if (!dst) {
     dst = DEFAULT_DST;
@@ -4063,19 +4063,14 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
             hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->fstream3, hipStreamNonBlocking, lo) == hipSuccess &&
-            (pool_mask.empty()
-                 ? hipStreamCreateWithPriority(&c->pool_st[0], hipStreamNonBlocking, hi) == hipSuccess &&
-                       hipStreamCreateWithPriority(&c->pool_st[1], hipStreamNonBlocking, hi) == hipSuccess
-                 : hipExtStreamCreateWithCUMask(&c->pool_st[0], (uint32_t)pool_mask.size(), pool_mask.data()) ==
-                           hipSuccess &&
-                       hipExtStreamCreateWithCUMask(&c->pool_st[1], (uint32_t)pool_mask.size(), pool_mask.data()) ==
-                           hipSuccess) &&
+            hipStreamCreateWithPriority(&c->pool_st[0], hipStreamNonBlocking, hi) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->pool_st[1], hipStreamNonBlocking, hi) == hipSuccess &&
             hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&
             hipMemset(c->result, 0, RES_WORDS * 4) == hipSuccess &&
             hipMalloc(&c->pool_q, (size_t)PQ_WORDS * 8) == hipSuccess && hipMemset(c->pool_q, 0, (size_t)PQ_WORDS * 8) == hipSuccess &&
             hipMalloc(&c->pool_desc, sizeof(PoolBatch) * OVH_BATCH_SLOTS) == hipSuccess &&
             hipMemset(c->pool_desc, 0, sizeof(PoolBatch) * OVH_BATCH_SLOTS) == hipSuccess &&
-            hipMalloc(&c->pool_scr, (size_t)2 * c->pool_wgs * VM_SLICES * VOTE_NSCR * 48) == hipSuccess &&
+            hipMalloc(&c->pool_scr, (size_t)4 * c->pool_wgs * VM_SLICES * VOTE_NSCR * 48) == hipSuccess &&
             hipHostMalloc((void**)&c->pool_err, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
   if (ok) *c->pool_err = 0;
@@ -5292,15 +5287,18 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
   // inputs are read in ovh_stream order (include/ovhip.h): waiting on `stream` here would also
   // wait for the previous batch's gather and combine queued there and serialise the pipeline
   // (r03b: 1,062k -> 796k verifs/s at one rank).
-  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes));
+  CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes, false, true, true));
   hipStream_t fst = c->fs[slot];
   int reg;
   uint32_t m;
   CHK(side_front(c, slot, 1, &reg, &m));
+  plog_stamp(c, slot, PLOG_EV_FOLD, fst);
   CHK(enqueue_msm(c, fst, slot, (uint32_t)n, d_codes));
+  plog_stamp(c, slot, PLOG_EV_MSM, fst);
   HIPCHK(hipEventRecord(c->ev_x[0], st));  // the caller's earlier work (a gather out of d_partial)
   HIPCHK(hipStreamWaitEvent(fst, c->ev_x[0], 0));
   k_pack_partial2<<<1, 64, 0, fst>>>(region_F(c, slot, reg), msm_S(c, slot), (uint32_t*)d_partial);
+  plog_stamp(c, slot, PLOG_EV_FINAL, fst);  // (here: the packed partial)
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(c->ev_x[1], fst));
   HIPCHK(hipStreamWaitEvent(st, c->ev_x[1], 0));
@@ -5405,6 +5403,7 @@ int ovh_combine_partials_device_async(ovh_ctx* c, size_t k, const uint8_t* d_par
   int32_t* verdict = c->result + RES_COMBINE + slot;
   enqueue_final(c, fst, F, S, m, verdict);
   if (n) enqueue_bisect(c, fst, slot, (uint32_t)n, d_codes, verdict);
+  plog_stamp(c, slot, PLOG_EV_BACK, fst);
   HIPCHK(hipEventRecord(c->ev_back[slot], fst));
   HIPCHK(hipGetLastError());
   return 0;

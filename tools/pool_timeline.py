@@ -89,6 +89,7 @@ def main():
     from consensus_overlord_amd.crypto import Context
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     runs = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    shard = len(sys.argv) > 3 and sys.argv[3] == "shard"
     c = Context(0, flags=bench.OVH_FLAG_PROFILE | bench.OVH_FLAG_VM_CLOCK)
     sks_h, hs_h = bench.synth_inputs(c.lib, 0, 4096)
     sks = torch.from_numpy(sks_h).cuda()
@@ -96,6 +97,24 @@ def main():
     pks = dev.sk_to_pk_batch(c, sks)
     sigs = dev.sign_batch(c, sks, hs)
     codes = torch.full((K + 2, 4096), -1, dtype=torch.int32, device="cuda")
+    if shard:   # the per-rank shard path at one rank (bench.py --shard-path): RCCL world of one
+        import torch.distributed as dist
+        from consensus_overlord_amd.shard import DeviceBackend, ShardVerifier
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        sv = ShardVerifier(DeviceBackend(c))
+        nsub = [0]
+
+        class dev:   # one_run's two calls over the shard driver
+            @staticmethod
+            def verify_batch_async(ctx, s_, h_, p_, cd):
+                sv.submit(nsub[0], s_, h_, p_, cd)
+                nsub[0] += 1
+
+            @staticmethod
+            def batch_wait(ctx):
+                sv.wait()
     for _ in range(runs):
         codes.fill_(-1)
         out = one_run(c, dev, sigs, hs, pks, K, codes)
