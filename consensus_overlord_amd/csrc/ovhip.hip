@@ -394,6 +394,16 @@ static_assert(POOL_SEQR > OVH_BATCH_SLOTS && POOL_SEQR / 2 <= POOL_QW, "pool que
 #define POOL_IDLE_TICKS 2000ull
 #define POOL_WAIT_TICKS 2000000ull
 
+// The SIMD a wave runs on, as a 12-bit key: XCC (3 bits) | SE (2) | SA (1) | CU (4) | SIMD (2) from
+// HW_REG_XCC_ID and HW_REG_HW_ID (amd_device_functions.h bit layout for gfx950); the pool log
+// records it per quad (ovh_pool_log, tools/pool_timeline.py)
+__device__ __forceinline__ uint32_t simd_key() {
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID, all 32 bits
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID bits 3:0
+  return (xcc & 7u) << 9 | ((hw >> 13) & 3u) << 7 | ((hw >> 12) & 1u) << 6 | ((hw >> 8) & 15u) << 2 |
+         ((hw >> 4) & 3u);
+}
+
 struct PoolBatch {  // one published batch (written by k_pool_publish, read by the pool)
   uint64_t seq;          // its sequence number (written last: a claimer checks it, pool_claim)
   uint32_t n, nq;
@@ -414,7 +424,7 @@ struct PoolBatch {  // one published batch (written by k_pool_publish, read by t
 
 // Pool log (OVH_FLAG_VM_CLOCK diagnostics, ovh_pool_log): a ring of PLOG_RING batch records of
 // PLOG_WORDS u64: [0..15] 100 MHz stamps of the batch's stream events (PLOG_EV_*) and its seq,
-// then per quad (< PLOG_QUADS) its start (bits 0..47) with the workgroup (bits 48..63) and end.
+// then per quad (< PLOG_QUADS) its start (bits 0..47) with the SIMD it ran on (simd_key, bits 48..63) and end.
 #define PLOG_RING 64u
 #define PLOG_QUADS 1024u
 #define PLOG_WORDS (16u + 2u * PLOG_QUADS)
@@ -744,7 +754,7 @@ __device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, u
   }
   if (uint64_t* pl = dgetp(&bd->plog); pl && threadIdx.x == 0 && quad < PLOG_QUADS) {
     const uint32_t* h3 = lds + SLOT_BASE_W + 3 * STRIDE + NSLOTS * 12 + 2;
-    pl[16 + 2 * quad] = ((uint64_t)h3[0] | (uint64_t)(h3[1] & 0xFFFFu) << 32) | (uint64_t)(blockIdx.x & 0xFFFFu) << 48;
+    pl[16 + 2 * quad] = ((uint64_t)h3[0] | (uint64_t)(h3[1] & 0xFFFFu) << 32) | (uint64_t)simd_key() << 48;
     pl[16 + 2 * quad + 1] = __builtin_amdgcn_s_memrealtime();
   }
 }
@@ -1041,12 +1051,20 @@ __global__ __launch_bounds__(64) void k_vm_votew(uint32_t n, VmDev prog, const u
 // u0, u1 | H | f (tools/fpvm/progs.py G_U, G_H, G_F).
 constexpr uint32_t VSAME_NSLOTS = VM_VSAME_NSLOTS > VM_VSAME_T_NSLOTS ? VM_VSAME_NSLOTS : VM_VSAME_T_NSLOTS;
 constexpr uint32_t VSAME_STRIDE_W = align256w(VSAME_NSLOTS * 12 + 4);
+// the 8-lane forms (programs vsame8 / vsame8_t: eight votes per wave) for batches of at least
+// VSAME8_MIN votes: 1,504 phases per eight votes against 1,288 per four, so a large batch's
+// per-vote waves take ~40% less SIMD time while a small one keeps the 16-lane form's latency
+constexpr uint32_t VSAME8_NSLOTS = VM_VSAME8_NSLOTS > VM_VSAME8_T_NSLOTS ? VM_VSAME8_NSLOTS : VM_VSAME8_T_NSLOTS;
+constexpr uint32_t VSAME8_STRIDE_W = align256w(VSAME8_NSLOTS * 12 + 4);
+#ifndef VSAME8_MIN
+#define VSAME8_MIN 2048u
+#endif
 constexpr uint32_t H2G_STRIDE_W = align256w(VM_H2G_NSLOTS * 12);
-static_assert(VM_VSAME_W == 16 && VM_VSAME_T_W == 16 && VM_H2G_W == 16 && VM_GMIL_W == 64 && VM_H2G_NIN == 4 &&
+static_assert(VM_VSAME_W == 16 && VM_VSAME_T_W == 16 && VM_VSAME8_W == 8 && VM_VSAME8_T_W == 8 && VM_H2G_W == 16 && VM_GMIL_W == 64 && VM_H2G_NIN == 4 &&
                   VM_GMIL_NIN == 9 && VM_G_U == 0 && VM_G_PLANES == 22,
               "same-message program shapes (tools/fpvm/progs.py)");
 
-// Per vote (16-lane slice, 4 per workgroup): votes lo + j, j < cnt (key bytes at pks + 48 j, or
+// Per vote (W-lane slice, 64 / W per workgroup; W = 16: vsame / vsame_t, 8: vsame8 / vsame8_t): votes lo + j, j < cnt (key bytes at pks + 48 j, or
 // table entry pk.idx[j]; signature at sigs + 96 j); stores sigma, tau and r pk at slab index
 // lo + j; code in the reference precedence without the H = O case (k_samemsg_fix adds it).
 // Same-message pipeline (r05ag/r05ah, tools/samemsg_pipe.py, 24 batches of 4,096 votes, ms per
@@ -1062,7 +1080,7 @@ static_assert(VM_VSAME_W == 16 && VM_VSAME_T_W == 16 && VM_H2G_W == 16 && VM_GMI
 #define SM_H2G_STREAMS 3
 #endif
 static_assert(SM_H2G_STREAMS >= 1 && SM_H2G_STREAMS <= 4, "hstream[4]");
-template <bool TABLE>
+template <bool TABLE, uint32_t W = 16>
 __global__ __launch_bounds__(64) void k_vm_vsame(uint32_t cnt, uint32_t lo, VmDev prog,
                                                  const uint32_t* __restrict__ cst_g, const uint8_t* __restrict__ pks,
                                                  PkSrc pk, const uint8_t* __restrict__ sigs, Slab s, uint64_t seed,
@@ -1071,12 +1089,16 @@ __global__ __launch_bounds__(64) void k_vm_vsame(uint32_t cnt, uint32_t lo, VmDe
   if (SM_PRIO) __builtin_amdgcn_s_setprio(2);
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   uint32_t* cst = lds;
-  const uint32_t slice = threadIdx.x / 16, lane = threadIdx.x % 16;
-  uint32_t* slots = lds + SLOT_BASE_W + slice * VSAME_STRIDE_W;
-  constexpr uint32_t NS = TABLE ? VM_VSAME_T_NSLOTS : VM_VSAME_NSLOTS;
+  static_assert(W == 16 || W == 8, "vsame slice width");
+  constexpr bool W8 = W == 8;
+  const uint32_t slice = threadIdx.x / W, lane = threadIdx.x % W;
+  uint32_t* slots = lds + SLOT_BASE_W + slice * (W8 ? VSAME8_STRIDE_W : VSAME_STRIDE_W);
+  constexpr uint32_t NS = W8 ? (TABLE ? VM_VSAME8_T_NSLOTS : VM_VSAME8_NSLOTS)
+                             : (TABLE ? VM_VSAME_T_NSLOTS : VM_VSAME_NSLOTS);
   uint32_t* hdr = slots + NS * 12;  // [sig flags, key flags]
-  const uint16_t* IN = TABLE ? VM_VSAME_T_IN : VM_VSAME_IN;
-  const uint32_t j = blockIdx.x * VM_SLICES + slice, i = lo + j;
+  const uint16_t* IN = W8 ? (TABLE ? VM_VSAME8_T_IN : VM_VSAME8_IN) : (TABLE ? VM_VSAME_T_IN : VM_VSAME_IN);
+  const uint16_t* OUT = W8 ? (TABLE ? VM_VSAME8_T_OUT : VM_VSAME8_OUT) : (TABLE ? VM_VSAME_T_OUT : VM_VSAME_OUT);
+  const uint32_t j = blockIdx.x * (64 / W) + slice, i = lo + j;
   const bool active = j < cnt;
   load_consts(cst, cst_g, VM_NCONST);
   if (active) {
@@ -1104,20 +1126,21 @@ __global__ __launch_bounds__(64) void k_vm_vsame(uint32_t cnt, uint32_t lo, VmDe
     }
   }
   __syncthreads();
-  vm::run(prog.code, TABLE ? VM_VSAME_T_NPHASES : VM_VSAME_NPHASES, 16, lane, active, slots, cst,
-          vote_scalar(seed, base, i), vm::Out{s.p, s.cap, i});
+  constexpr uint32_t NPH = W8 ? (TABLE ? VM_VSAME8_T_NPHASES : VM_VSAME8_NPHASES)
+                              : (TABLE ? VM_VSAME_T_NPHASES : VM_VSAME_NPHASES);
+  vm::run(prog.code, NPH, W, lane, active, slots, cst, vote_scalar(seed, base, i), vm::Out{s.p, s.cap, i});
   if (active && lane == 0) {
     const uint32_t sf = hdr[0], pf = hdr[1];
     const uint32_t sg_bad = sf & 1, sg_inf = (sf >> 1) & 1, sg_xz = (sf >> 2) & 1;
     uint32_t kf = pf, sg_ok, sg_grp;
     if constexpr (TABLE) {
-      sg_ok = slot_flag_get(slots, VM_VSAME_T_OUT[VM_VSAME_T_OUT_SIG_OK]);
-      sg_grp = slot_flag_get(slots, VM_VSAME_T_OUT[VM_VSAME_T_OUT_SIG_GRP]);
+      sg_ok = slot_flag_get(slots, OUT[VM_VSAME_T_OUT_SIG_OK]);
+      sg_grp = slot_flag_get(slots, OUT[VM_VSAME_T_OUT_SIG_GRP]);
     } else {
-      sg_ok = slot_flag_get(slots, VM_VSAME_OUT[VM_VSAME_OUT_SIG_OK]);
-      sg_grp = slot_flag_get(slots, VM_VSAME_OUT[VM_VSAME_OUT_SIG_GRP]);
-      const uint32_t pk_ok = slot_flag_get(slots, VM_VSAME_OUT[VM_VSAME_OUT_PK_OK]);
-      const uint32_t pk_grp = slot_flag_get(slots, VM_VSAME_OUT[VM_VSAME_OUT_PK_GRP]);
+      sg_ok = slot_flag_get(slots, OUT[VM_VSAME_OUT_SIG_OK]);
+      sg_grp = slot_flag_get(slots, OUT[VM_VSAME_OUT_SIG_GRP]);
+      const uint32_t pk_ok = slot_flag_get(slots, OUT[VM_VSAME_OUT_PK_OK]);
+      const uint32_t pk_grp = slot_flag_get(slots, OUT[VM_VSAME_OUT_PK_GRP]);
       const uint32_t pk_bad = pf & 1, pk_inf = (pf >> 1) & 1, pk_xz = (pf >> 2) & 1;
       kf = (pk_bad || (!pk_inf && (!pk_ok || pk_xz))) ? PKF_PARSE : pk_inf ? PKF_INF : !pk_grp ? PKF_GRP : 0u;
     }
@@ -2393,7 +2416,7 @@ struct ovh_ctx {
   // Fp-VM programs + constant table in device memory
   // same-message batches (verify_samemsg_locked): programs, per slot the group slab (G_PLANES
   // planes + the H-is-infinity words, gcap entries); OVH_SAMEMSG=0 turns the path off
-  VmDev vm_vsame{}, vm_vsame_t{}, vm_h2g{}, vm_gmil{}, vm_pkdec{}, vm_g1grp{}, vm_gfin{};
+  VmDev vm_vsame{}, vm_vsame_t{}, vm_vsame8{}, vm_vsame8_t{}, vm_h2g{}, vm_gmil{}, vm_pkdec{}, vm_g1grp{}, vm_gfin{};
   uint32_t* gslab[OVH_BATCH_SLOTS] = {};
   uint32_t gcap[OVH_BATCH_SLOTS] = {};
   // 0: off; 1 (default): batches above small_max votes (below it the small-batch path has the
@@ -2488,6 +2511,8 @@ static_assert(LDS_RS <= 64 * 1024 && LDS_MSM8 <= 64 * 1024 && LDS_HDBL <= 64 * 1
               "default LDS limit");
 static_assert(LDS_VOTE <= 160 * 1024 && LDS_VOTE_T <= 160 * 1024 && LDS_FINAL <= 160 * 1024, "VM LDS budget");
 static constexpr size_t LDS_VSAME = ((size_t)SLOT_BASE_W + VM_SLICES * (size_t)VSAME_STRIDE_W) * 4;
+static constexpr size_t LDS_VSAME8 = ((size_t)SLOT_BASE_W + 8 * (size_t)VSAME8_STRIDE_W) * 4;
+static_assert(LDS_VSAME8 <= 64 * 1024, "vsame8 LDS (default limit)");
 static constexpr size_t LDS_H2G = ((size_t)SLOT_BASE_W + VM_SLICES * (size_t)H2G_STRIDE_W) * 4;
 static constexpr size_t LDS_GMIL = ((size_t)SLOT_BASE_W + (size_t)VM_GMIL_NSLOTS * 12) * 4;
 static_assert(LDS_VSAME <= 64 * 1024 && LDS_H2G <= 64 * 1024 && LDS_GMIL + 16 <= 64 * 1024, "same-message LDS");
@@ -2623,6 +2648,10 @@ static int vm_init(ovh_ctx* c) {
                 VM_VSAME_OUT, VM_VSAME_NOUT));
   CHK(vm_upload(c, c->vm_vsame_t, VM_VSAME_T_CODE, VM_VSAME_T_NPHASES, VM_VSAME_T_W, VM_VSAME_T_NW, VM_VSAME_T_IN,
                 VM_VSAME_T_NIN, VM_VSAME_T_OUT, VM_VSAME_T_NOUT));
+  CHK(vm_upload(c, c->vm_vsame8, VM_VSAME8_CODE, VM_VSAME8_NPHASES, VM_VSAME8_W, VM_VSAME8_NW, VM_VSAME8_IN,
+                VM_VSAME8_NIN, VM_VSAME8_OUT, VM_VSAME8_NOUT));
+  CHK(vm_upload(c, c->vm_vsame8_t, VM_VSAME8_T_CODE, VM_VSAME8_T_NPHASES, VM_VSAME8_T_W, VM_VSAME8_T_NW, VM_VSAME8_T_IN,
+                VM_VSAME8_T_NIN, VM_VSAME8_T_OUT, VM_VSAME8_T_NOUT));
   CHK(vm_upload(c, c->vm_h2g, VM_H2G_CODE, VM_H2G_NPHASES, VM_H2G_W, VM_H2G_NW, VM_H2G_IN, VM_H2G_NIN, VM_H2G_OUT,
                 VM_H2G_NOUT));
   CHK(vm_upload(c, c->vm_gfin, VM_GFIN_CODE, VM_GFIN_NPHASES, VM_GFIN_W, VM_GFIN_NW, VM_GFIN_IN, VM_GFIN_NIN, VM_GFIN_OUT,
@@ -3502,12 +3531,21 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   const PkSrc tab{c->tab.planes, c->tab.cap, c->tab.flags, tidx};
   {
     StageScope p(c, ST_VOTE, st);
-    if (T)
-      k_vm_vsame<true><<<(T + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(T, 0, c->vm_vsame_t, c->vm_consts, nullptr,
-                                                                              tab, sigs, s, seed, base, dc);
-    if (N > T)
-      k_vm_vsame<false><<<(N - T + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(
-          N - T, T, c->vm_vsame, c->vm_consts, pks, PkSrc{}, sigs + 96 * (size_t)T, s, seed, base, dc);
+    if (N >= VSAME8_MIN) {  // eight votes per wave (VSAME8_MIN)
+      if (T)
+        k_vm_vsame<true, 8><<<(T + 7) / 8, 64, LDS_VSAME8, st>>>(T, 0, c->vm_vsame8_t, c->vm_consts, nullptr, tab, sigs,
+                                                                 s, seed, base, dc);
+      if (N > T)
+        k_vm_vsame<false, 8><<<(N - T + 7) / 8, 64, LDS_VSAME8, st>>>(
+            N - T, T, c->vm_vsame8, c->vm_consts, pks, PkSrc{}, sigs + 96 * (size_t)T, s, seed, base, dc);
+    } else {
+      if (T)
+        k_vm_vsame<true><<<(T + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(T, 0, c->vm_vsame_t, c->vm_consts,
+                                                                                nullptr, tab, sigs, s, seed, base, dc);
+      if (N > T)
+        k_vm_vsame<false><<<(N - T + VM_SLICES - 1) / VM_SLICES, 64, LDS_VSAME, st>>>(
+            N - T, T, c->vm_vsame, c->vm_consts, pks, PkSrc{}, sigs + 96 * (size_t)T, s, seed, base, dc);
+    }
   }
   HIPCHK(hipEventRecord(c->ev_front[slot], st));
   HIPCHK(hipStreamWaitEvent(fst, c->ev_front[slot], 0));
@@ -4056,13 +4094,16 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   }
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
+#ifndef OVH_FIN_PRIO
+#define OVH_FIN_PRIO(lo, hi) (lo)
+#endif
   // streams: ovh_stream (normal priority), three final streams (lowest), the two pool streams
   // (highest; created with the context, so each holds a hardware queue of its own)
   bool ok = xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream3, hipStreamNonBlocking, lo) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, OVH_FIN_PRIO(lo, hi)) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, OVH_FIN_PRIO(lo, hi)) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream3, hipStreamNonBlocking, OVH_FIN_PRIO(lo, hi)) == hipSuccess &&
             hipStreamCreateWithPriority(&c->pool_st[0], hipStreamNonBlocking, hi) == hipSuccess &&
             hipStreamCreateWithPriority(&c->pool_st[1], hipStreamNonBlocking, hi) == hipSuccess &&
             hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&

@@ -36,17 +36,18 @@ WIDTH.update({"sigchk": 16, "pkchk": 16, "g1padd": 8, "vote1": 64, "vote_t1": 64
 # same-message batches (r04): per vote a 16-lane slice, per distinct hash one 16-lane slice for
 # hash_to_G2 and one wave for its Miller loop (the latency of a round's group)
 WIDTH.update({"vsame": 16, "vsame_t": 16, "h2g": 16, "gmil": 64, "pkdec": 4, "g1grp": 16, "gfin": 64})
-MAX_SLOTS = {"gfin": 2048, "vsame": 400, "vsame_t": 400, "h2g": 400, "gmil": 1200, "vote": 200, "vote_t": 200, "fold": 256, "final": 2048, "final1": 2048, "vote1": 1200, "vote_t1": 1200,
+WIDTH.update({"vsame8": 8, "vsame8_t": 8})   # large same-message batches: eight votes per wave
+MAX_SLOTS = {"gfin": 2048, "vsame": 400, "vsame_t": 400, "vsame8": 400, "vsame8_t": 400, "h2g": 400, "gmil": 1200, "vote": 200, "vote_t": 200, "fold": 256, "final": 2048, "final1": 2048, "vote1": 1200, "vote_t1": 1200,
              "votew": 1200, "votew_t": 1200, "qcpre": 1200, "qcmil": 1200, "vote1h": 1200, "vote_t1h": 1200}
 # phases an op may run ahead of its first consumer's earliest start (sched.schedule `hoist`)
-HOIST = {"gfin": 50, "vsame": 250, "vsame_t": 250, "h2g": 250, "gmil": 250, "vote": 250, "vote_t": 250, "final": 50, "vote1": 250, "vote_t1": 250, "final1": 50, "votew": 250,
+HOIST = {"gfin": 50, "vsame": 250, "vsame_t": 250, "vsame8": 250, "vsame8_t": 250, "h2g": 250, "gmil": 250, "vote": 250, "vote_t": 250, "final": 50, "vote1": 250, "vote_t1": 250, "final1": 50, "votew": 250,
          "votew_t": 250, "qcpre": 250, "qcmil": 250, "vote1h": 250, "vote_t1h": 250}
-STRETCH = {"gfin": 1.0, "vsame": 1.0, "vsame_t": 1.0, "h2g": 1.0, "gmil": 1.0, "final": 1.0, "vote": 1.0, "vote_t": 1.0, "vote1": 1.0, "vote_t1": 1.0, "final1": 1.0, "votew": 1.0,
+STRETCH = {"gfin": 1.0, "vsame": 1.0, "vsame_t": 1.0, "vsame8": 1.0, "vsame8_t": 1.0, "h2g": 1.0, "gmil": 1.0, "final": 1.0, "vote": 1.0, "vote_t": 1.0, "vote1": 1.0, "vote_t1": 1.0, "final1": 1.0, "votew": 1.0,
            "votew_t": 1.0, "qcpre": 1.0, "qcmil": 1.0, "vote1h": 1.0, "vote_t1h": 1.0}
 # priority weight of a heavy op against a light one (path length in weighted ops). r03 scan on
 # the cost model (product phase 1.60 us, linear 0.69 us): vote 4 -> 64 estimates 3.29 -> 3.10 ms
 # (a product on the path outweighs any run of light ops); vote_t keeps 2
-HEAVY_W = {"vote": 64, "vsame": 64, "vsame_t": 64, "h2g": 64}
+HEAVY_W = {"vote": 64, "vsame": 64, "vsame_t": 64, "vsame8": 64, "vsame8_t": 64, "h2g": 64}
 # list-scheduling priority offsets per program section (ir.Prog.section): the signature's
 # decompression + subgroup check has no successor, so by path length alone it loses every
 # contended phase to the Miller loop and ends up as a latency-bound tail; the offset runs it in
@@ -63,7 +64,7 @@ SEC_BIAS = {"vote_t": {"sig": 1500}}
 # slots would outgrow the LDS budget).
 NOMIX = set(filter(None, os.environ.get(
     "OVH_GEN_NOMIX", "vote,vote_t,vote1,vote_t1,vote1h,vote_t1h,final1,qcpre,qcmil,votew,votew_t,signg0,signg1,"
-    "sigchk,pkchk,pkgen,vsame,vsame_t,h2g,gmil,pkdec,g1grp").split(",")))
+    "sigchk,pkchk,pkgen,vsame,vsame_t,vsame8,vsame8_t,h2g,gmil,pkdec,g1grp").split(",")))
 # r04: the batch vote programs keep at most SPILL_K values in LDS per phase; the rest wait in the
 # vote's global scratch (sched.spill_pass: side-word spills / fills beside the lane ops), so a
 # CU holds seven vote workgroups -- two pipelined batches' grids co-resident -- beside a final
@@ -309,6 +310,9 @@ def check_samemsg(built, bls, g):
         assert sched.simulate(tsc, twords, tin, r) == tgot, "vsame_t: simulated"
         Xt, Yt, Zt = (tgot["st:r%d" % j] for j in range(3))
         assert (Xt * pow(Zt, -1, P) % P, Yt * pow(Zt, -1, P) % P) == rP, "vsame_t: r pk"
+        for nm, vi, want in (("vsame8", vin, got), ("vsame8_t", tin, tgot)):   # the 8-lane schedules
+            _, sc8, w8, _, _ = built[nm]
+            assert sched.simulate(sc8, w8, vi, r) == want, nm + ": simulated"
         hprog, hsc, hwords, hins, _ = built["h2g"]
         hin = {n: inp[n] for n in hins}
         hv = hprog.evaluate(hin)

@@ -50,12 +50,27 @@ def one_run(c, dev, sigs, hs, pks, K, codes):
         en = q[:, 1].astype(np.int64)
         ok = (st > 0) & (en > 0)
         st, en = st[ok], en[ok]
+        key = (q[:, 0] >> 48).astype(np.int64)[ok]   # the SIMD the quad ran on (simd_key)
+        _, inv, per = np.unique(key, return_inverse=True, return_counts=True)
+        _, cinv, cper = np.unique(key >> 2, return_inverse=True, return_counts=True)
+        dur = (en - st) / 100.0
+        # quad time by how many of the batch's quads shared its SIMD / its CU
+        by_simd = {int(k): round(float(np.median(dur[per[inv] == k])), 1) for k in np.unique(per)}
+        by_cu = {int(k): [int((cper[cinv] == k).sum()), round(float(np.median(dur[cper[cinv] == k])), 1)]
+                 for k in np.unique(cper)}
         spans.append(np.stack([st, en], 1))
         ev = {EV[k]: round((int(a[r, k]) - t_base) / 100.0, 1) if a[r, k] else None for k in range(len(EV))}
         rows.append({"seq": int(seqs[r]), **ev,
                      "q_first": round((int(st.min()) - t_base) / 100.0, 1),
                      "q_last": round((int(en.max()) - t_base) / 100.0, 1),
-                     "quad_us_med": round(float(np.median(en - st)) / 100.0, 1), "quads": int(ok.sum())})
+                     "quad_us_med": round(float(np.median(en - st)) / 100.0, 1), "quads": int(ok.sum()),
+                     "simds": len(per), "quads_per_simd_max": int(per.max()) if len(per) else 0,
+                     "quad_us_pct": [round(float(np.percentile(dur, p_)), 1) for p_ in (1, 10, 50, 90, 99, 100)],
+                     "quad_us_by_simd_share": by_simd, "quads_and_us_by_cu_share": by_cu,
+                     # the slowest 1%: (us, quads on its SIMD, on its CU, start after the first)
+                     "slowest": [(round(float(dur[k]), 1), int(per[inv][k]), int(cper[cinv][k]),
+                                  round((int(st[k]) - int(st.min())) / 100.0, 1))
+                                 for k in np.argsort(-dur)[:max(1, len(dur) // 100)]]})
     sp = np.concatenate(spans)
     t_end = int(sp[:, 1].max())
     grid = np.arange(t_base, t_end, 10000)  # every 100 us
