@@ -4094,16 +4094,13 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   }
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = numerically largest = lowest priority
-#ifndef OVH_FIN_PRIO
-#define OVH_FIN_PRIO(lo, hi) (lo)
-#endif
   // streams: ovh_stream (normal priority), three final streams (lowest), the two pool streams
   // (highest; created with the context, so each holds a hardware queue of its own)
   bool ok = xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) &&
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, OVH_FIN_PRIO(lo, hi)) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, OVH_FIN_PRIO(lo, hi)) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream3, hipStreamNonBlocking, OVH_FIN_PRIO(lo, hi)) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
+            hipStreamCreateWithPriority(&c->fstream3, hipStreamNonBlocking, lo) == hipSuccess &&
             hipStreamCreateWithPriority(&c->pool_st[0], hipStreamNonBlocking, hi) == hipSuccess &&
             hipStreamCreateWithPriority(&c->pool_st[1], hipStreamNonBlocking, hi) == hipSuccess &&
             hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&
