@@ -380,8 +380,10 @@ enum : uint32_t {
   PQ_DONE = 4 * POOL_QW,
   PQ_CLAIM = PQ_DONE + OVH_BATCH_SLOTS * POOL_QW,
   PQ_INFL = PQ_CLAIM + OVH_BATCH_SLOTS * POOL_QW,  // quads claimed and not yet done (all batches)
+  PQ_OCC = PQ_INFL + POOL_QW,  // POOL_OCC_N uint32: pool quads running on each SIMD (simd_key)
 };
-constexpr uint32_t PQ_WORDS = PQ_INFL + POOL_QW;
+constexpr uint32_t POOL_OCC_N = 4096;
+constexpr uint32_t PQ_WORDS = PQ_OCC + POOL_OCC_N / 2;
 static_assert(POOL_SEQR > OVH_BATCH_SLOTS && POOL_SEQR / 2 <= POOL_QW, "pool queue layout");
 // A workgroup that finds the queue empty polls it for POOL_IDLE_TICKS (20 us) before it exits --
 // or, while a batch is announced but not yet published (nann > npub: its staging and
@@ -403,6 +405,13 @@ __device__ __forceinline__ uint32_t simd_key() {
   return (xcc & 7u) << 9 | ((hw >> 13) & 3u) << 7 | ((hw >> 12) & 1u) << 6 | ((hw >> 8) & 15u) << 2 |
          ((hw >> 4) & 3u);
 }
+__device__ __forceinline__ uint32_t* pq_occ(uint64_t* q) { return reinterpret_cast<uint32_t*>(q + PQ_OCC); }
+// SIMD spreading: while the current batch is the last published and its unclaimed quads fit the
+// SIMDs that run no pool quad (estimate: SIMDs - quads in flight), a workgroup whose SIMD already
+// runs a pool quad leaves the claim to one on an idle SIMD for up to POOL_SPREAD_TICKS (200 us):
+// a lone batch's 1,024 quads then take 1,024 SIMDs (two quads on a SIMD take 4.6-5.6 ms, one
+// 3.8, r05az) -- with the pool's grids dealt one wave per SIMD (pool_grid0)
+#define POOL_SPREAD_TICKS 20000ull
 
 struct PoolBatch {  // one published batch (written by k_pool_publish, read by the pool)
   uint64_t seq;          // its sequence number (written last: a claimer checks it, pool_claim)
@@ -471,6 +480,8 @@ struct PoolArgs {
   uint64_t* wlog;  // OVH_FLAG_VM_CLOCK: this grid's workgroup log (PLOG_WG_WORDS per workgroup), else null
   uint64_t only;   // ~0: claim any batch; else this grid's own batch: its workgroups leave once
                    // `cur` has passed it (the shard path's grid per batch, ovh_batch_partial_device)
+  uint32_t nsimd;  // SIMDs of the device (SIMD spreading, pool_claim)
+  uint32_t pad;
 };
 
 __device__ __forceinline__ uint64_t* pq_done(uint64_t* q, uint32_t slot) { return q + PQ_DONE + slot * POOL_QW; }
@@ -518,6 +529,11 @@ __device__ __forceinline__ uint64_t lane0_fetch_add(uint64_t* p, uint64_t v) {
   return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32) |
          __builtin_amdgcn_readfirstlane((uint32_t)r);
 }
+__device__ __forceinline__ uint32_t lane0_fetch_add32(uint32_t* p, uint32_t v) {
+  uint32_t r = 0;
+  if (threadIdx.x == 0) r = __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __builtin_amdgcn_readfirstlane(r);
+}
 __device__ __forceinline__ void lane0_cas(uint64_t* p, uint64_t expect, uint64_t want) {
   if (threadIdx.x == 0) {
     uint64_t e = expect;
@@ -534,8 +550,9 @@ __device__ __forceinline__ uint64_t qldu(const uint64_t* p) {
   return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 __device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* slot_out, uint32_t* quad_out,
-                               uint32_t* why, uint64_t only) {
-  uint64_t t0 = wclock();
+                               uint32_t* why, uint64_t only, uint32_t nsimd) {
+  uint64_t t0 = wclock(), tdef = 0;
+  uint32_t* occ = pq_occ(q) + simd_key();
   *why = 3;
 #pragma unroll 1
   for (uint32_t tries = 0; tries < (1u << 22); ++tries) {
@@ -556,6 +573,36 @@ __device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* sl
     }
     const uint32_t slot = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load(pq_slot_of(q) + s % POOL_SEQR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    // SIMD spreading: this SIMD's occupancy is taken first (one fetch-add, so two workgroups of a
+    // SIMD polling the same publication cannot both see it idle), then the claim is deferred
+    // while the SIMD was busy
+    bool held = false;
+    if (np == s + 1) {
+      bool busy;
+      if (tdef && __builtin_amdgcn_readfirstlane(__hip_atomic_load(occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        busy = true;  // deferring: a plain load while the SIMD stays busy
+      } else {
+        busy = lane0_fetch_add32(occ, 1u) != 0;
+        held = true;
+      }
+      if (busy) {
+        const uint64_t cw = qldu(pq_claim(q, slot));
+        const uint32_t nq = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&descs[slot].nq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const uint64_t infl = qldu(q + PQ_INFL);
+        const uint32_t taken = (uint32_t)cw;
+        if ((cw >> 32) == s && taken < nq && (uint64_t)(nq - taken) + infl <= nsimd) {
+          const uint64_t now = wclock();
+          if (!tdef) tdef = now;
+          if (now - tdef < POOL_SPREAD_TICKS) {
+            if (held) (void)lane0_fetch_add32(occ, ~0u);
+            __builtin_amdgcn_s_sleep(32);
+            continue;
+          }
+        }
+      }
+    }
+    if (!held) (void)lane0_fetch_add32(occ, 1u);
     const uint64_t old = lane0_fetch_add(pq_claim(q, slot), 1ull);
     const uint64_t seq = old >> 32;
     const uint32_t idx = (uint32_t)old;
@@ -579,6 +626,8 @@ __device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* sl
       *quad_out = idx;
       return 1;
     }
+    (void)lane0_fetch_add32(occ, ~0u);  // - 1: no quad after all
+    tdef = 0;
     t0 = wclock();  // progress: the idle window restarts
   }
   return 0;
@@ -751,6 +800,7 @@ __device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, u
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(pq_done(a.q, slot), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(a.q + PQ_INFL, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // - 1
+    __hip_atomic_fetch_add(pq_occ(a.q) + simd_key(), ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (uint64_t* pl = dgetp(&bd->plog); pl && threadIdx.x == 0 && quad < PLOG_QUADS) {
     const uint32_t* h3 = lds + SLOT_BASE_W + 3 * STRIDE + NSLOTS * 12 + 2;
@@ -774,7 +824,7 @@ __global__ __launch_bounds__(64, 2) void k_vm_pool(PoolArgs a) {
 #pragma unroll 1
   for (;; ++nquads) {
     uint32_t slot = 0, quad = 0;
-    if (!pool_claim(a.q, a.descs, &slot, &quad, &why, a.only)) break;
+    if (!pool_claim(a.q, a.descs, &slot, &quad, &why, a.only, a.nsimd)) break;
     slot = uni(slot);
     quad = uni(quad);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this batch's descriptor and inputs, fresh
@@ -2346,6 +2396,8 @@ struct ovh_ctx {
   void* pool_desc = nullptr;
   uint32_t* pool_scr = nullptr;
   uint32_t pool_wgs = 0;
+  uint32_t pool_grid0 = 0;
+  uint32_t ncu = 256;  // workgroups of pool stream 0's grid (4 per CU); stream 1's: 2 pool_wgs - it
   uint64_t pool_seq = 0;
   uint32_t* pool_err = nullptr;
   uint64_t* plog = nullptr;  // OVH_FLAG_VM_CLOCK: the pool log (PLOG_RING records)
@@ -2957,6 +3009,8 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   const uint32_t wgs = c->pool_wgs;
   PoolArgs pa;
   pa.only = ~0ull;
+  pa.nsimd = 4 * c->ncu;
+  pa.pad = 0;
   pa.q = c->pool_q;
   pa.descs = (const PoolBatch*)c->pool_desc;
   pa.pv_code = c->vm_vote.code;
@@ -2977,16 +3031,17 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
       if (c->flags & OVH_FLAG_PROFILE) HIPCHK(hipEventRecord(c->ev0[ST_VOTE], pst));
       if (vev) HIPCHK(hipEventRecord(c->vev0[vk], pst));
     }
-    // each workgroup's own scratch: grid par's workgroups at par x (its size): the two streams'
-    // grids may be co-resident (a shard grid is twice the size)
-    pa.scr = c->pool_scr + (size_t)par * (shard ? 2 : 1) * c->pool_wgs * VM_SLICES * VOTE_NSCR * 12;
+    // each workgroup's own scratch: grid 1's after grid 0's (the two streams' grids may be
+    // co-resident; a shard grid is the whole pool, at par x its size)
+    const uint32_t gw = shard ? 2 * wgs : par == 0 ? c->pool_grid0 : 2 * wgs - c->pool_grid0;
+    pa.scr = c->pool_scr + (size_t)(shard ? par * 2 * wgs : par * c->pool_grid0) * VM_SLICES * VOTE_NSCR * 12;
     pa.wlog = nullptr;
     if (c->plog) {  // grid record: [seq, par, workgroups, -], then the workgroups'
       uint64_t* g = c->plog + PLOG_GRID_BASE + (size_t)(c->plog_grids++ % PLOG_GRIDS) * (4 + PLOG_WGS * PLOG_WG_WORDS);
-      k_grid_hdr<<<1, 64, 0, pst>>>(g, seq, par, shard ? 2 * wgs : wgs);
+      k_grid_hdr<<<1, 64, 0, pst>>>(g, seq, par, gw);
       pa.wlog = g + 4;
     }
-    k_vm_pool<<<shard ? 2 * wgs : wgs, 64, LDS_POOL, pst>>>(pa);
+    k_vm_pool<<<gw, 64, LDS_POOL, pst>>>(pa);
     if (par == 1 || shard) {
       if (c->flags & OVH_FLAG_PROFILE) {
         HIPCHK(hipEventRecord(c->ev1[ST_VOTE], pst));
@@ -4088,6 +4143,12 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   // side by side: each grid holds half of them
   c->pool_wgs = ((uint32_t)ncu * 8 - (uint32_t)ncu * POOL_HOLES_PER_8CU / 8) / 2;
   if (c->pool_wgs > POOL_MAX_WGS) c->pool_wgs = POOL_MAX_WGS;
+  // the two grids as 4 + 3 workgroups per CU rather than 3.5 + 3.5: a grid of a whole number of
+  // workgroups per CU is dealt evenly (one per SIMD), so every SIMD holds a pool wave -- with two
+  // half-pools some CUs got 8 and others 6, some SIMDs none, and a lone batch's quads doubled up
+  // on ~90 SIMDs (5.6 ms against 3.8 for a quad alone, r05az)
+  c->pool_grid0 = std::min(4u * (uint32_t)ncu, 2 * c->pool_wgs - 1);
+  c->ncu = (uint32_t)ncu;
   if (!dst) {
     dst = DEFAULT_DST;
     dst_len = 43;
