@@ -1,9 +1,4 @@
 set -e
-O=gpurun_out/$1; mkdir -p $O; shift
-L=$PWD/consensus_overlord_amd
-B="timeout -k 10 200 python -u bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-latency --clock-seconds 0"
-for i in 1 2 3; do
-  for v in "$@"; do
-    if [ "$v" = base ]; then $B > $O/${v}_$i.log 2>&1; else OVH_LIBPATH=$L/libovhip_$v.so $B > $O/${v}_$i.log 2>&1; fi
-  done
-done
+TAG=$1 TESTS=1 SMOKE=1 BENCH=1 PROF=1 STEPS=30 bash tools/gpu.sh
+timeout -k 10 120 python -u tools/pool_timeline.py 1 3 > gpurun_out/$1/tl1.json 2> gpurun_out/$1/tl1.err
+timeout -k 10 200 python -u bench.py --steps 30 --warmup 2 --no-cpu-baseline --no-latency --clock-seconds 0 --shard-path > gpurun_out/$1/shard.log 2>&1
