@@ -550,8 +550,9 @@ __device__ __forceinline__ uint64_t qldu(const uint64_t* p) {
   return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 __device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* slot_out, uint32_t* quad_out,
-                               uint32_t* why, uint64_t only, uint32_t nsimd) {
+                               uint32_t* why, uint64_t only, uint32_t nsimd, uint32_t* how) {
   uint64_t t0 = wclock(), tdef = 0;
+  uint32_t hw = 0;  // how the claim went (pool log): 1 last published, 2 SIMD busy, 4 deferred, 8 busy and not deferred
   uint32_t* occ = pq_occ(q) + simd_key();
   *why = 3;
 #pragma unroll 1
@@ -578,6 +579,7 @@ __device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* sl
     // while the SIMD was busy
     bool held = false;
     if (np == s + 1) {
+      hw |= 1u;
       bool busy;
       if (tdef && __builtin_amdgcn_readfirstlane(__hip_atomic_load(occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
         busy = true;  // deferring: a plain load while the SIMD stays busy
@@ -586,20 +588,25 @@ __device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* sl
         held = true;
       }
       if (busy) {
+        hw |= 2u;
         const uint64_t cw = qldu(pq_claim(q, slot));
         const uint32_t nq = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(&descs[slot].nq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         const uint64_t infl = qldu(q + PQ_INFL);
         const uint32_t taken = (uint32_t)cw;
-        if ((cw >> 32) == s && taken < nq && (uint64_t)(nq - taken) + infl <= nsimd) {
+        // (a slack of nsimd / 16: at nsimd exactly, a lone batch's late arrivals claimed next to a
+        // running quad instead of deferring -- pool-log claim flags 11, r05bj)
+        if ((cw >> 32) == s && taken < nq && (uint64_t)(nq - taken) + infl <= nsimd + nsimd / 16) {
           const uint64_t now = wclock();
           if (!tdef) tdef = now;
           if (now - tdef < POOL_SPREAD_TICKS) {
+            hw |= 4u;
             if (held) (void)lane0_fetch_add32(occ, ~0u);
             __builtin_amdgcn_s_sleep(32);
             continue;
           }
         }
+        hw |= 8u;
       }
     }
     if (!held) (void)lane0_fetch_add32(occ, 1u);
@@ -624,6 +631,7 @@ __device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* sl
       (void)lane0_fetch_add(q + PQ_INFL, 1ull);
       *slot_out = slot;
       *quad_out = idx;
+      *how = hw;
       return 1;
     }
     (void)lane0_fetch_add32(occ, ~0u);  // - 1: no quad after all
@@ -673,7 +681,7 @@ __device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, u
   uint32_t* park = lds + SLOT_BASE_W + 2 * STRIDE + NSLOTS * 12 + 2;  // slice 2's hdr[2..3]
   {
     const PoolBatch* bd = a.descs + slot_in;
-    const uint32_t i = quad_in * VM_SLICES + slice;
+    const uint32_t i = (quad_in & 0x0FFFFFFFu) * VM_SLICES + slice;  // (top bits: the claim flags)
     const uint32_t n = uni(dget(&bd->n));
     const bool active = i < n;
     const uint8_t* sigs = unip(dgetp(&bd->stage));
@@ -740,7 +748,7 @@ __device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, u
                   a.scr + (size_t)blockIdx.x * VM_SLICES * VOTE_NSCR * 12 + slice * VOTE_NSCR * 12);
   }
   // after the program: the slot and quad back from LDS (run ends with an LDS wait + barrier)
-  const uint32_t slot = uni(park[0]), quad = uni(park[1]);
+  const uint32_t slot = uni(park[0]), quad = uni(park[1]) & 0x0FFFFFFFu, how = uni(park[1]) >> 28;
   const PoolBatch* bd = a.descs + slot;
   const uint32_t i = quad * VM_SLICES + slice;
   const uint32_t n = uni(dget(&bd->n));
@@ -804,7 +812,8 @@ __device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, u
   }
   if (uint64_t* pl = dgetp(&bd->plog); pl && threadIdx.x == 0 && quad < PLOG_QUADS) {
     const uint32_t* h3 = lds + SLOT_BASE_W + 3 * STRIDE + NSLOTS * 12 + 2;
-    pl[16 + 2 * quad] = ((uint64_t)h3[0] | (uint64_t)(h3[1] & 0xFFFFu) << 32) | (uint64_t)simd_key() << 48;
+    pl[16 + 2 * quad] = ((uint64_t)h3[0] | (uint64_t)(h3[1] & 0xFFFFu) << 32) | (uint64_t)simd_key() << 48 |
+                        (uint64_t)how << 60;
     pl[16 + 2 * quad + 1] = __builtin_amdgcn_s_memrealtime();
   }
 }
@@ -823,10 +832,10 @@ __global__ __launch_bounds__(64, 2) void k_vm_pool(PoolArgs a) {
   uint32_t nquads = 0, why = 0;
 #pragma unroll 1
   for (;; ++nquads) {
-    uint32_t slot = 0, quad = 0;
-    if (!pool_claim(a.q, a.descs, &slot, &quad, &why, a.only, a.nsimd)) break;
+    uint32_t slot = 0, quad = 0, how = 0;
+    if (!pool_claim(a.q, a.descs, &slot, &quad, &why, a.only, a.nsimd, &how)) break;
     slot = uni(slot);
-    quad = uni(quad);
+    quad = uni(quad) | uni(how) << 28;  // the claim's flags ride in the top bits to the pool log
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this batch's descriptor and inputs, fresh
     if (uni(dget(&a.descs[slot].table))) vote_quad<true>(a, slot, quad, lds);
     else vote_quad<false>(a, slot, quad, lds);

@@ -50,7 +50,8 @@ def one_run(c, dev, sigs, hs, pks, K, codes):
         en = q[:, 1].astype(np.int64)
         ok = (st > 0) & (en > 0)
         st, en = st[ok], en[ok]
-        key = (q[:, 0] >> 48).astype(np.int64)[ok]   # the SIMD the quad ran on (simd_key)
+        key = ((q[:, 0] >> 48) & 0xFFF).astype(np.int64)[ok]   # the SIMD the quad ran on (simd_key)
+        how = (q[:, 0] >> 60).astype(np.int64)[ok]   # the claim's flags (pool_claim)
         _, inv, per = np.unique(key, return_inverse=True, return_counts=True)
         _, cinv, cper = np.unique(key >> 2, return_inverse=True, return_counts=True)
         dur = (en - st) / 100.0
@@ -65,6 +66,8 @@ def one_run(c, dev, sigs, hs, pks, K, codes):
                      "q_last": round((int(en.max()) - t_base) / 100.0, 1),
                      "quad_us_med": round(float(np.median(en - st)) / 100.0, 1), "quads": int(ok.sum()),
                      "simds": len(per), "quads_per_simd_max": int(per.max()) if len(per) else 0,
+                     "claim_flags": {int(k): int(v) for k, v in zip(*np.unique(how, return_counts=True))},
+                     "claim_flags_doubled": {int(k): int(v) for k, v in zip(*np.unique(how[per[inv] > 1], return_counts=True))},
                      "quad_us_pct": [round(float(np.percentile(dur, p_)), 1) for p_ in (1, 10, 50, 90, 99, 100)],
                      "quad_us_by_simd_share": by_simd, "quads_and_us_by_cu_share": by_cu,
                      # the slowest 1%: (us, quads on its SIMD, on its CU, start after the first)
