@@ -433,7 +433,8 @@ struct PoolBatch {  // one published batch (written by k_pool_publish, read by t
 
 // Pool log (OVH_FLAG_VM_CLOCK diagnostics, ovh_pool_log): a ring of PLOG_RING batch records of
 // PLOG_WORDS u64: [0..15] 100 MHz stamps of the batch's stream events (PLOG_EV_*) and its seq,
-// then per quad (< PLOG_QUADS) its start (bits 0..47) with the SIMD it ran on (simd_key, bits 48..63) and end.
+// then per quad (< PLOG_QUADS) its start (bits 0..47) with the SIMD it ran on (simd_key, bits 48..59), the
+// claim flags (pool_claim, bits 60..63) and end.
 #define PLOG_RING 64u
 #define PLOG_QUADS 1024u
 #define PLOG_WORDS (16u + 2u * PLOG_QUADS)

@@ -288,7 +288,8 @@ int ovh_vm_clock(ovh_ctx* ctx, uint64_t* stamps, size_t max);
 /* Diagnostics (context created with OVH_FLAG_VM_CLOCK): the vote pool's log, a ring of 64 batch
  * records of 2,064 words -- 100 MHz stamps of the batch's stream events (publication, pool done,
  * folds, MSM, final, bisection; word 15 its sequence number), then per quad (< 1,024) its start
- * (bits 0..47; bits 48..63 the SIMD it ran on: XCC, SE, SA, CU, SIMD as 3+2+1+4+2 bits) and end. Copies up to `max` words after synchronising;
+ * (bits 0..47; bits 48..59 the SIMD it ran on: XCC, SE, SA, CU, SIMD as 3+2+1+4+2 bits; bits 60..63 how
+ * its claim went: 1 last published batch, 2 its SIMD busy, 4 deferred, 8 busy and not deferred) and end. Copies up to `max` words after synchronising;
  * returns the log's size in words (0 without the flag, <0 on error). */
 int ovh_pool_log(ovh_ctx* ctx, uint64_t* words, size_t max);
 
