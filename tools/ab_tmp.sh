@@ -1,3 +1,3 @@
 set -e
-TAG=$1 TESTS=1 SMOKE=1 BENCH=1 PROF=1 STEPS=30 bash tools/gpu.sh
-timeout -k 10 200 python -u bench.py --steps 30 --warmup 2 --no-cpu-baseline --no-latency --clock-seconds 0 --shard-path > gpurun_out/$1/shard.log 2>&1
+O=gpurun_out/$1; mkdir -p $O
+timeout -k 10 150 python -u tools/pool_timeline.py 1 6 > $O/tl1.json 2> $O/tl1.err
