@@ -47,7 +47,7 @@
 #ifdef OVH_VM_PROGS
 #include OVH_VM_PROGS  // A/B builds: another generation of the programs
 #else
-#include "vm_progs.inc"
+#include <vm_progs.inc>  // generated (tools/fpvm/gen.py): -Icsrc (Makefile) or -I OUT_DIR (overlord-hip/build.rs)
 #endif
 static_assert(VM_KZERO == ovh::vm::KZERO && VM_KTAB == ovh::vm::KTAB, "fixed constants (tools/fpvm/gen.py)");
 
@@ -797,25 +797,32 @@ __device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, u
   // visible to the workgroup first; the fold reuses the vote slots' LDS.
   __threadfence();
   __syncthreads();
+  // the pool log's pointer and the quad's start stamp (slice 3's LDS header) into registers now:
+  // fold_unit reuses the slot LDS, and once done reaches nq the slot may carry the next batch
+  // 
+  uint64_t* const pl = threadIdx.x == 0 && quad < PLOG_QUADS ? dgetp(&bd->plog) : nullptr;
+  uint64_t pl_start = 0;
+  if (pl) {
+    const uint32_t* h3 = lds + SLOT_BASE_W + 3 * STRIDE + NSLOTS * 12 + 2;
+    pl_start = (uint64_t)h3[0] | (uint64_t)(h3[1] & 0xFFFFu) << 32;
+  }
   const Slab s{unip(dgetp(&bd->state)), uni(dget(&bd->cap))};
   VmDev fold{};
   fold.code = a.fold_code;
   fold_unit(quad, n, fold, cst, lds + SLOT_BASE_W, threadIdx.x % VM_FOLD_W, threadIdx.x < VM_FOLD_W,
             Slab{s.p + (size_t)S_F * 12 * s.cap, s.cap}, Slab{nullptr, 0},
             Slab{unip(dgetp(&bd->part0)), uni(dget(&bd->part_cap))}, codes);
-  // the quad's codes, planes and partial, then its done count (k_pool_wait)
+  if (pl) {  // the quad's pool-log record, ahead of the release below
+    pl[16 + 2 * quad] = pl_start | (uint64_t)simd_key() << 48 | (uint64_t)how << 60;
+    pl[16 + 2 * quad + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+  // the quad's codes, planes, partial and log record, then its done count (k_pool_wait)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(pq_done(a.q, slot), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(a.q + PQ_INFL, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // - 1
     __hip_atomic_fetch_add(pq_occ(a.q) + simd_key(), ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (uint64_t* pl = dgetp(&bd->plog); pl && threadIdx.x == 0 && quad < PLOG_QUADS) {
-    const uint32_t* h3 = lds + SLOT_BASE_W + 3 * STRIDE + NSLOTS * 12 + 2;
-    pl[16 + 2 * quad] = ((uint64_t)h3[0] | (uint64_t)(h3[1] & 0xFFFFu) << 32) | (uint64_t)simd_key() << 48 |
-                        (uint64_t)how << 60;
-    pl[16 + 2 * quad + 1] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -2777,8 +2784,63 @@ static Slab region_S(ovh_ctx* c, int slot, int r) {
               c->red_cap};
 }
 
-// Every stream of the context idle; OVH_ERR_DEVICE when a final stream gave up waiting for the
-// vote pool (k_pool_wait: its batch's results are not trustworthy).
+// ---- streams
+// A context's streams are never destroyed: ovh_destroy synchronises them and parks them here,
+// per device and priority, and the next context created on that device takes them back. A
+// caller may have recorded events of its own on a context's stream (torch's pinned-host
+// allocator does so for every non-blocking copy from pinned memory issued on
+// torch.cuda.ExternalStream(ctx.stream)) and query them after ovh_destroy; an event recorded on
+// a destroyed stream dereferences the freed queue when it is queried (the r05ab segfault, in the
+// test's teardown, after Context.close(): VERDICT r05). Parked streams keep every such event
+// valid for the life of the process; the number of streams is bounded by the most contexts ever
+// alive at once. include/ovhip.h states the contract.
+namespace {
+struct ParkedStream {
+  int device;
+  int prio;
+  hipStream_t s;
+};
+std::mutex g_park_mu;
+std::vector<ParkedStream> g_parked;
+}  // namespace
+
+// A non-blocking stream of priority `prio` on the current device (a parked one if any).
+static hipError_t stream_new(hipStream_t* s, int prio) {
+  int dev = 0;
+  const hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  {
+    std::lock_guard<std::mutex> g(g_park_mu);
+    for (size_t k = 0; k < g_parked.size(); ++k)
+      if (g_parked[k].device == dev && g_parked[k].prio == prio) {
+        *s = g_parked[k].s;
+        g_parked.erase(g_parked.begin() + (ptrdiff_t)k);
+        return hipSuccess;
+      }
+  }
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, prio);
+}
+
+// Park stream s of `device` (its work drained first).
+static void stream_park(int device, hipStream_t s) {
+  if (!s) return;
+  (void)hipStreamSynchronize(s);
+  int prio = 0;
+  if (hipStreamGetPriority(s, &prio) != hipSuccess) return;  // (never destroyed either way)
+  std::lock_guard<std::mutex> g(g_park_mu);
+  g_parked.push_back(ParkedStream{device, prio, s});
+}
+
+// OVH_ERR_DEVICE once a final stream gave up waiting for the vote pool (k_pool_wait: that batch's
+// partial, verdict and codes are not trustworthy). The flag is sticky: the pool queue may still
+// hold the batch, so the context stays failed until ovh_destroy (include/ovhip.h). Every
+// synchronous return that hands out results derived from a pool batch checks it after its
+// synchronisation.
+static int pool_failed(const ovh_ctx* c) {
+  return c->pool_err && __atomic_load_n(c->pool_err, __ATOMIC_ACQUIRE) ? OVH_ERR_DEVICE : 0;
+}
+
+// Every stream of the context idle, then the pool check above.
 static int sync_all(ovh_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipStreamSynchronize(c->fstream));
@@ -2787,8 +2849,7 @@ static int sync_all(ovh_ctx* c) {
   for (hipStream_t s : {c->pool_st[0], c->pool_st[1], c->vstream[0], c->vstream[1], c->vstream[2], c->hstream[1],
                         c->hstream[2], c->hstream[3]})
     if (s) HIPCHK(hipStreamSynchronize(s));
-  if (c->pool_err && __atomic_load_n(c->pool_err, __ATOMIC_ACQUIRE)) return OVH_ERR_DEVICE;
-  return 0;
+  return pool_failed(c);
 }
 
 // MSM scratch of a slot (msm.hpp MsmArgs), in words: cnt, off, cur, level prefixes, entries
@@ -3041,10 +3102,13 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
       if (c->flags & OVH_FLAG_PROFILE) HIPCHK(hipEventRecord(c->ev0[ST_VOTE], pst));
       if (vev) HIPCHK(hipEventRecord(c->vev0[vk], pst));
     }
-    // each workgroup's own scratch: grid 1's after grid 0's (the two streams' grids may be
-    // co-resident; a shard grid is the whole pool, at par x its size)
+    // each workgroup's own scratch: one fixed region of 2 x wgs workgroups per pool stream, for
+    // every grid shape (a normal grid or a shard grid of the whole pool). Grids of one stream run
+    // one after the other; grids of the two streams may be co-resident -- including a normal grid
+    // and a shard grid when a caller mixes the APIs without ovh_batch_wait -- and
+    // never share a workgroup's spill area
     const uint32_t gw = shard ? 2 * wgs : par == 0 ? c->pool_grid0 : 2 * wgs - c->pool_grid0;
-    pa.scr = c->pool_scr + (size_t)(shard ? par * 2 * wgs : par * c->pool_grid0) * VM_SLICES * VOTE_NSCR * 12;
+    pa.scr = c->pool_scr + (size_t)par * 2 * wgs * VM_SLICES * VOTE_NSCR * 12;
     pa.wlog = nullptr;
     if (c->plog) {  // grid record: [seq, par, workgroups, -], then the workgroups'
       uint64_t* g = c->plog + PLOG_GRID_BASE + (size_t)(c->plog_grids++ % PLOG_GRIDS) * (4 + PLOG_WGS * PLOG_WG_WORDS);
@@ -3563,7 +3627,7 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
       if (!*v) {
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        HIPCHK(hipStreamCreateWithPriority(v, hipStreamNonBlocking, hi));
+        HIPCHK(stream_new(v, hi));
       }
     st = pair[c->pipe_k & 1];
   }
@@ -3575,11 +3639,11 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   // queues and serialised them (r04m trace), and on ovh_stream it delayed the next batch's
   // per-vote work (r04n), so the one-hash path runs on three high-priority streams (a pool of
   // their own: the two per-vote streams and this one) and the final streams (its key sums there).
-  if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+  if (!c->xstream) HIPCHK(stream_new(&c->xstream, 0));
   // hash_to_G2 of the one-hash API: SM_H2G_STREAMS streams in turn (one wave each; on a single
   // stream consecutive batches' hash_to_G2 ran back to back)
   const uint32_t hk = one ? (uint32_t)(c->pipe_k % SM_H2G_STREAMS) : 0u;
-  if (hk && !c->hstream[hk]) HIPCHK(hipStreamCreateWithFlags(&c->hstream[hk], hipStreamNonBlocking));
+  if (hk && !c->hstream[hk]) HIPCHK(stream_new(&c->hstream[hk], 0));
   const hipStream_t xs = one ? fst : c->xstream, hs = hk ? c->hstream[hk] : c->xstream;
   HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));  // the inputs (and the slot free: take_slot)
   HIPCHK(hipStreamWaitEvent(hs, c->ev_front[slot], 0));
@@ -4168,12 +4232,12 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   // streams: ovh_stream (normal priority), three final streams (lowest), the two pool streams
   // (highest; created with the context, so each holds a hardware queue of its own)
   bool ok = xmd_build_templates(c->xmd, dst, (uint32_t)dst_len) &&
-            hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream2, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->fstream3, hipStreamNonBlocking, lo) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->pool_st[0], hipStreamNonBlocking, hi) == hipSuccess &&
-            hipStreamCreateWithPriority(&c->pool_st[1], hipStreamNonBlocking, hi) == hipSuccess &&
+            stream_new(&c->stream, 0) == hipSuccess &&
+            stream_new(&c->fstream, lo) == hipSuccess &&
+            stream_new(&c->fstream2, lo) == hipSuccess &&
+            stream_new(&c->fstream3, lo) == hipSuccess &&
+            stream_new(&c->pool_st[0], hi) == hipSuccess &&
+            stream_new(&c->pool_st[1], hi) == hipSuccess &&
             hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&
             hipMemset(c->result, 0, RES_WORDS * 4) == hipSuccess &&
             hipMalloc(&c->pool_q, (size_t)PQ_WORDS * 8) == hipSuccess && hipMemset(c->pool_q, 0, (size_t)PQ_WORDS * 8) == hipSuccess &&
@@ -4310,10 +4374,10 @@ static void destroy_one(ovh_ctx* c) {
     if (c->vev0[k]) (void)hipEventDestroy(c->vev0[k]);
     if (c->vev1[k]) (void)hipEventDestroy(c->vev1[k]);
   }
-  if (c->stream) (void)hipStreamDestroy(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
-                        c->pool_st[1], c->hstream[1], c->hstream[2], c->hstream[3]})
-    if (s) (void)hipStreamDestroy(s);
+  // the streams are parked, not destroyed (stream_new)
+  for (hipStream_t s : {c->stream, c->fstream, c->fstream2, c->fstream3, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
+                        c->pool_st[0], c->pool_st[1], c->hstream[1], c->hstream[2], c->hstream[3]})
+    stream_park(c->device, s);
   if (c->pool_err) (void)hipHostFree(c->pool_err);
   delete c;
 }
@@ -4344,7 +4408,7 @@ int ovh_diag_vm_occupancy(ovh_ctx* c, int prog, size_t n, int reps, int streams,
   CHK(ensure_cap(c, n));
   CHK(ensure_in(c, n * 180 + 64));
   CHK(sync_all(c));
-  if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+  if (!c->xstream) HIPCHK(stream_new(&c->xstream, 0));
   HIPCHK(hipMemsetAsync(c->in_buf, 0, n * 180, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   const Slab s{c->state_slot[0], c->cap};
@@ -4735,7 +4799,7 @@ int ovh_aggregate_sigs(ovh_ctx* c, const uint8_t* sigs, const size_t* sig_lens, 
     HIPCHK(hipEventRecord(c->ev_x[2], c->stream));  // staged inputs
     // created on first use: a context that only verifies batches keeps to three streams, which
     // map onto distinct hardware queues at HIP's default of four (GPU_MAX_HW_QUEUES)
-    if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+    if (!c->xstream) HIPCHK(stream_new(&c->xstream, 0));
     HIPCHK(hipStreamWaitEvent(c->xstream, c->ev_x[2], 0));
     bool keys48 = true;
     for (size_t i = 0; i < n; ++i) keys48 = keys48 && pk_lens[i] == 48;
@@ -4952,7 +5016,7 @@ static int verify_aggregated_vm(ovh_ctx* c, const uint8_t* agg_sig, size_t agg_l
   c->last_n = 0;
   Slab s{c->state_slot[slot], c->cap};
   HIPCHK(hipEventRecord(c->ev_x[2], c->stream));  // staged inputs
-  if (!c->xstream) HIPCHK(hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking));
+  if (!c->xstream) HIPCHK(stream_new(&c->xstream, 0));
   HIPCHK(hipStreamWaitEvent(c->xstream, c->ev_x[2], 0));
   k_h2f<<<1, WG, 0, c->xstream>>>(1, d + n * 48 + 96, c->xmd, s);
   k_vm_qcpre<<<1, 64, LDS_QCPRE, c->xstream>>>(c->vm_qcpre, c->vm_consts, d + n * 48, s, qpf);
@@ -5388,7 +5452,7 @@ int ovh_batch_partial_device(ovh_ctx* c, size_t n, const uint8_t* d_sigs, const 
     CHK(batch_front(c, slot, (uint32_t)n, d_sigs, d_hashes, KeySrc{d_pks, PkSrc{}}, d_codes));
     CHK(shard_partial(c, slot, (uint32_t)n, d_codes, (uint32_t*)d_partial, nullptr));
     HIPCHK(hipStreamSynchronize(c->stream));
-    return 0;
+    return pool_failed(c);  // (the partial of a timed-out pool wait is stale)
   }
   // pipelined: only the staging, hash_to_field and the publication on the main stream (the votes
   // in the pool); the fold levels, the MSM and the packing on the slot's final stream, which the
@@ -5472,6 +5536,8 @@ int ovh_combine_partials_device(ovh_ctx* c, size_t k, const uint8_t* d_partials,
   int32_t r = -1;
   HIPCHK(hipMemcpyAsync(&r, c->result + RES_SYNC, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  *verdict = 0;
+  CHK(pool_failed(c));  // partials of this context's timed-out batch may be among the inputs
   *verdict = r == 1 ? 1 : 0;
   return 0;
 }
@@ -5486,7 +5552,7 @@ int ovh_batch_fallback_device(ovh_ctx* c, size_t n, int32_t* d_codes) {
   enqueue_bisect(c, c->stream, c->last_slot, (uint32_t)n, d_codes, nullptr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));
-  return 0;
+  return pool_failed(c);
 }
 
 int ovh_combine_partials_device_async(ovh_ctx* c, size_t k, const uint8_t* d_partials, size_t n, int32_t* d_codes,

@@ -40,6 +40,9 @@ typedef struct ovh_ctx ovh_ctx;
 #define OVH_ERR_LEN_MISMATCH 101
 #define OVH_ERR_PUBKEY 102
 #define OVH_ERR_ARG 103
+/* A HIP error, or a batch's final stream gave up waiting for the vote pool. The latter is
+ * sticky: every later synchronising call of the context (ovh_batch_wait, the synchronous batch
+ * and partial / combine / fallback entry points) returns it, and the context must be destroyed. */
 #define OVH_ERR_DEVICE 200
 #define OVH_ERR_RNG 201
 
@@ -72,6 +75,12 @@ ovh_ctx* ovh_create_multi(const int* devices, int ndev, const uint8_t* dst, size
  * device count), or OVH_ERR_ARG when cap < n * n. The pipelined combined check
  * (ovh_verify_batch_async) rotates over the devices with peer access to and from every other. */
 int ovh_multi_peer_matrix(ovh_ctx* ctx, uint8_t* out, size_t cap);
+/* Synchronises every stream of the context and frees its device memory. The streams themselves
+ * are not destroyed: they are parked per device and priority and handed to later contexts of
+ * that device, so an ovh_stream handle -- and any event a caller recorded on it, e.g. torch's
+ * pinned-host allocator after a non-blocking copy issued on ExternalStream(ovh_stream(ctx)) --
+ * stays valid for the life of the process. Work a caller enqueued on ovh_stream before
+ * ovh_destroy completes before the call returns. */
 void ovh_destroy(ovh_ctx* ctx);
 /* Number of devices of the context (1 for ovh_create). */
 int ovh_device_count(ovh_ctx* ctx);

@@ -5,19 +5,34 @@
 //! selects it by config (`crypto_backend = "hip"` beside `src/config.rs:18-31`); nothing else in
 //! the node changes. The arithmetic runs on the GPU (gfx950 HIP kernels); there is no CPU path.
 //!
+//! Like `ConsensusCrypto` (`#[derive(Clone)]`, consensus.rs:339) it is cheap to clone:
+//! `Consensus::new` clones it into `Brain`, into the `Arc` overlord holds and into itself
+//! (consensus.rs:61-76). The clones share one device context (`Arc<Ctx>`: the last clone to drop
+//! destroys it, never twice) and one key list, as the reference's clones share
+//! `Arc<RwLock<Vec<BlsPublicKey>>>`. `update_pubkeys` is `async` and takes the reference callers'
+//! `Vec<BlsPublicKey>` (consensus.rs:131-136, :622-629) through ophelia's `PublicKey` trait.
+//!
 //! Error mapping (reference `src/error.rs:20-44`, `consensus.rs:391-462`): code 100 is
 //! `Other("failed to convert hash value")`, 101 `Other("signatures length does not match voters
 //! length")`, 102 `Other("lose public key")`, 1..=7 a blst error (`CryptoErr`), anything else a
-//! device error. Overlord only observes Ok / Err.
+//! device error. The variants and their Display follow the reference's `ConsensusError`
+//! (derive_more `{_0:?}` / `"Crypto error {_0:?}"`); overlord only observes Ok / Err.
+//!
+//! Not compiled in this repository's image (no Rust toolchain): `tests/test_crate_ffi.py` checks
+//! the FFI block against the header and the drop-in shape (Clone, `update_pubkeys`, the ingress
+//! module's calls) textually.
 pub mod ffi;
+pub mod ingress;
 
 use bytes::Bytes;
 use overlord::Crypto as OverlordCrypto;
 use std::error::Error;
 use std::fmt;
-use std::sync::Mutex;
+use std::sync::atomic::{AtomicI32, Ordering};
+use std::sync::Arc;
+use tokio::sync::RwLock;
 
-/// The reference's `ConsensusError` variants this backend can return.
+/// The reference's `ConsensusError` variants this backend can return (`src/error.rs:20-44`).
 #[derive(Debug)]
 pub enum HipCryptoError {
     /// `ConsensusError::Other(String)`: hash length, list length mismatch, key parse.
@@ -31,8 +46,8 @@ pub enum HipCryptoError {
 impl fmt::Display for HipCryptoError {
     fn fmt(&self, f: &mut fmt::Formatter<'_>) -> fmt::Result {
         match self {
-            HipCryptoError::Other(s) => write!(f, "{s}"),
-            HipCryptoError::CryptoErr(c) => write!(f, "blst error {c}"),
+            HipCryptoError::Other(s) => write!(f, "{s:?}"),
+            HipCryptoError::CryptoErr(c) => write!(f, "Crypto error {c:?}"),
             HipCryptoError::Device(c) => write!(f, "hip device error {c}"),
         }
     }
@@ -40,8 +55,15 @@ impl fmt::Display for HipCryptoError {
 
 impl Error for HipCryptoError {}
 
-fn to_err(code: i32) -> Box<dyn Error + Send> {
-    Box::new(match code {
+/// As the reference's `impl From<ConsensusError> for Box<dyn Error + Send>` (error.rs:41-45).
+impl From<HipCryptoError> for Box<dyn Error + Send> {
+    fn from(error: HipCryptoError) -> Self {
+        Box::new(error) as Box<dyn Error + Send>
+    }
+}
+
+pub(crate) fn to_err(code: i32) -> Box<dyn Error + Send> {
+    match code {
         ffi::OVH_ERR_HASH_LEN => HipCryptoError::Other("failed to convert hash value".into()),
         ffi::OVH_ERR_LEN_MISMATCH => {
             HipCryptoError::Other("signatures length does not match voters length".into())
@@ -49,10 +71,11 @@ fn to_err(code: i32) -> Box<dyn Error + Send> {
         ffi::OVH_ERR_PUBKEY => HipCryptoError::Other("lose public key".into()),
         1..=7 => HipCryptoError::CryptoErr(code),
         c => HipCryptoError::Device(c),
-    })
+    }
+    .into()
 }
 
-fn check(code: i32) -> Result<(), Box<dyn Error + Send>> {
+pub(crate) fn check(code: i32) -> Result<(), Box<dyn Error + Send>> {
     if code == ffi::OVH_OK {
         Ok(())
     } else {
@@ -65,7 +88,10 @@ fn concat(v: &[Bytes]) -> (Vec<u8>, Vec<usize>) {
     (v.iter().flat_map(|b| b.iter().copied()).collect(), v.iter().map(|b| b.len()).collect())
 }
 
-struct Ctx(*mut ffi::OvhCtx);
+/// The device context. Owned through `Arc` by every clone of `HipCrypto` (and by the blocking
+/// tasks `update_pubkeys` and the ingress shim start); `ovh_destroy` runs once, when the last
+/// owner drops it.
+pub(crate) struct Ctx(pub(crate) *mut ffi::OvhCtx);
 // libovhip serialises every entry point on the context's own mutex (include/ovhip.h: the trait
 // object is Send + Sync and is called by overlord and the check_block handler concurrently).
 unsafe impl Send for Ctx {}
@@ -77,14 +103,19 @@ impl Drop for Ctx {
     }
 }
 
-/// The GPU `Crypto` of a node: its private key (as `ConsensusCrypto::new` reads it) and the name
-/// (48-byte compressed public key).
+/// The GPU `Crypto` of a node: its private key (as `ConsensusCrypto::new` reads it), the name
+/// (48-byte compressed public key) and the validator keys (`ConsensusCrypto::pubkeys`).
+#[derive(Clone)]
 pub struct HipCrypto {
-    ctx: Ctx,
-    private_key: Vec<u8>,
+    ctx: Arc<Ctx>,
+    private_key: Arc<Vec<u8>>,
     pub name: Bytes,
-    // serialises the (rare) reconfiguration against itself; device work is serialised by libovhip
-    pubkeys: Mutex<Vec<Bytes>>,
+    /// The validator keys as last given to `update_pubkeys` (the device table holds them
+    /// decompressed and group-checked); shared by every clone, as the reference's field.
+    pub pubkeys: Arc<RwLock<Vec<Bytes>>>,
+    /// The code of the last failed device table upload (0: none); `update_pubkeys` returns
+    /// nothing, as the reference's does.
+    table_error: Arc<AtomicI32>,
 }
 
 impl HipCrypto {
@@ -115,37 +146,91 @@ impl HipCrypto {
             ffi::ovh_sk_to_pk(ctx.0, private_key.as_ptr(), private_key.len(), name.as_mut_ptr())
         })?;
         Ok(HipCrypto {
-            ctx,
-            private_key,
+            ctx: Arc::new(ctx),
+            private_key: Arc::new(private_key),
             name: Bytes::copy_from_slice(&name),
-            pubkeys: Mutex::new(Vec::new()),
+            pubkeys: Arc::new(RwLock::new(Vec::new())),
+            table_error: Arc::new(AtomicI32::new(0)),
         })
     }
 
-    /// `ConsensusCrypto::update_pubkeys` (consensus.rs:361-363; callers :131-136, :622-629): the
-    /// validator keys go to the device table (decompressed and group-checked once).
-    pub fn update_pubkeys(&self, keys: Vec<Bytes>) -> Result<(), Box<dyn Error + Send>> {
-        let mut held = self.pubkeys.lock().unwrap();
-        let flat: Vec<u8> = keys.iter().flat_map(|k| k.iter().copied()).collect();
-        if keys.iter().any(|k| k.len() != 48) {
-            return Err(to_err(ffi::OVH_ERR_PUBKEY));
-        }
-        check(unsafe { ffi::ovh_set_validators(self.ctx.0, flat.as_ptr(), keys.len()) })?;
-        *held = keys;
-        Ok(())
+    pub(crate) fn raw(&self) -> *mut ffi::OvhCtx {
+        self.ctx.0
     }
 
-    /// The vote-batching hook at `proc_network_msg` (consensus.rs:210-262): batch-verify held
-    /// votes; later `verify_signature` calls on them are answered from the verdict cache.
-    /// Call from `spawn_blocking`, never on the reactor.
+    /// `ConsensusCrypto::update_pubkeys` (consensus.rs:361-363), same shape: `async`, no result,
+    /// takes the callers' `Vec<BlsPublicKey>` (consensus.rs:131-136, :622-629) -- any ophelia
+    /// `PublicKey`. The keys go to the device table (decompressed and group-checked once, on a
+    /// blocking task: never on the reactor). A key the device cannot parse stays in the table as
+    /// unparsed, and a vote by it answers "lose public key" exactly as the key path does; a
+    /// failed upload leaves the table empty (every vote then takes the key path, still exact)
+    /// and is reported by `table_error`.
+    pub async fn update_pubkeys<K: ophelia::PublicKey>(&self, new_pubkeys: Vec<K>) {
+        let keys: Vec<Bytes> = new_pubkeys.iter().map(|k| k.to_bytes()).collect();
+        let ctx = self.ctx.clone();
+        let n = keys.len();
+        let all48 = keys.iter().all(|k| k.len() == 48);
+        let flat: Vec<u8> = keys.iter().flat_map(|k| k.iter().copied()).collect();
+        let code = tokio::task::spawn_blocking(move || {
+            if all48 {
+                unsafe { ffi::ovh_set_validators(ctx.0, flat.as_ptr(), n) }
+            } else {
+                // not compressed G1 keys: an empty table (the key path serves every vote)
+                let c = unsafe { ffi::ovh_set_validators(ctx.0, std::ptr::null(), 0) };
+                if c == ffi::OVH_OK {
+                    ffi::OVH_ERR_PUBKEY
+                } else {
+                    c
+                }
+            }
+        })
+        .await
+        .unwrap_or(ffi::OVH_ERR_DEVICE);
+        self.table_error.store(code, Ordering::Relaxed);
+        *self.pubkeys.write().await = keys;
+    }
+
+    /// The code of the last failed `update_pubkeys` upload (0 when the table is current).
+    pub fn table_error(&self) -> i32 {
+        self.table_error.load(Ordering::Relaxed)
+    }
+
+    /// The vote-batching hook at `proc_network_msg` (consensus.rs:210-262, `ingress::VoteIngress`):
+    /// batch-verify held votes; later `verify_signature` calls on them are answered from the
+    /// verdict cache. Blocking: call from `spawn_blocking`, never on the reactor.
     pub fn prefetch(&self, sigs: &[[u8; 96]], hashes: &[[u8; 32]], voters: &[[u8; 48]]) -> Result<(), Box<dyn Error + Send>> {
         if sigs.len() != hashes.len() || sigs.len() != voters.len() {
             return Err(to_err(ffi::OVH_ERR_LEN_MISMATCH));
         }
         check(unsafe {
-            ffi::ovh_prefetch(self.ctx.0, sigs.len(), sigs.as_ptr() as *const u8, hashes.as_ptr() as *const u8,
+            ffi::ovh_prefetch(self.raw(), sigs.len(), sigs.as_ptr() as *const u8, hashes.as_ptr() as *const u8,
                               voters.as_ptr() as *const u8)
         })
+    }
+
+    /// hash(rlp(Vote)) of n votes on the device (`ovh_vote_digests`: rlp + SM3 per vote, the
+    /// bytes overlord signs, consensus.rs:169-175). `block_hashes` holds one hash per vote of at
+    /// most OVH_VOTE_HASH_MAX bytes. Blocking.
+    pub fn vote_digests(&self, heights: &[u64], rounds: &[u64], vote_types: &[u8], block_hashes: &[Bytes]) -> Result<Vec<[u8; 32]>, Box<dyn Error + Send>> {
+        let n = heights.len();
+        if rounds.len() != n || vote_types.len() != n || block_hashes.len() != n {
+            return Err(to_err(ffi::OVH_ERR_LEN_MISMATCH));
+        }
+        let mut hb = vec![0u8; n * ffi::OVH_VOTE_HASH_MAX];
+        let mut hl = vec![0u8; n];
+        for (i, h) in block_hashes.iter().enumerate() {
+            if h.len() > ffi::OVH_VOTE_HASH_MAX {
+                return Err(to_err(ffi::OVH_ERR_ARG));
+            }
+            hb[i * ffi::OVH_VOTE_HASH_MAX..i * ffi::OVH_VOTE_HASH_MAX + h.len()].copy_from_slice(h);
+            hl[i] = h.len() as u8;
+        }
+        let mut out = vec![[0u8; 32]; n];
+        check(unsafe {
+            ffi::ovh_vote_digests(self.raw(), n, heights.as_ptr(), rounds.as_ptr(), vote_types.as_ptr(), hb.as_ptr(),
+                                  hl.as_ptr(), out.as_mut_ptr() as *mut u8)
+        })?;
+        Ok(out)
     }
 
     /// n x `verify_signature` in one call: codes[i] is the per-call code of vote i (0 = Ok).
@@ -155,7 +240,7 @@ impl HipCrypto {
         }
         let mut codes = vec![0i32; sigs.len()];
         check(unsafe {
-            ffi::ovh_verify_batch(self.ctx.0, sigs.len(), sigs.as_ptr() as *const u8, hashes.as_ptr() as *const u8,
+            ffi::ovh_verify_batch(self.raw(), sigs.len(), sigs.as_ptr() as *const u8, hashes.as_ptr() as *const u8,
                                   voters.as_ptr() as *const u8, codes.as_mut_ptr())
         })?;
         Ok(codes)
@@ -174,7 +259,7 @@ impl OverlordCrypto for HipCrypto {
     fn sign(&self, hash: Bytes) -> Result<Bytes, Box<dyn Error + Send>> {
         let mut out = [0u8; 96];
         check(unsafe {
-            ffi::ovh_sign(self.ctx.0, self.private_key.as_ptr(), self.private_key.len(), hash.as_ptr(), hash.len(),
+            ffi::ovh_sign(self.raw(), self.private_key.as_ptr(), self.private_key.len(), hash.as_ptr(), hash.len(),
                           out.as_mut_ptr())
         })?;
         Ok(Bytes::copy_from_slice(&out))
@@ -183,7 +268,7 @@ impl OverlordCrypto for HipCrypto {
     /// consensus.rs:397-416: hash length (100), pk parse (102), sig parse (1..3), verify (3, 5, 6).
     fn verify_signature(&self, signature: Bytes, hash: Bytes, voter: Bytes) -> Result<(), Box<dyn Error + Send>> {
         check(unsafe {
-            ffi::ovh_verify(self.ctx.0, signature.as_ptr(), signature.len(), hash.as_ptr(), hash.len(),
+            ffi::ovh_verify(self.raw(), signature.as_ptr(), signature.len(), hash.as_ptr(), hash.len(),
                             voter.as_ptr(), voter.len())
         })
     }
@@ -195,7 +280,7 @@ impl OverlordCrypto for HipCrypto {
         let (v, vl) = concat(&voters);
         let mut out = [0u8; 96];
         check(unsafe {
-            ffi::ovh_aggregate_sigs(self.ctx.0, s.as_ptr(), sl.as_ptr(), sl.len(), v.as_ptr(), vl.as_ptr(), vl.len(),
+            ffi::ovh_aggregate_sigs(self.raw(), s.as_ptr(), sl.as_ptr(), sl.len(), v.as_ptr(), vl.as_ptr(), vl.len(),
                                     out.as_mut_ptr())
         })?;
         Ok(Bytes::copy_from_slice(&out))
@@ -206,7 +291,7 @@ impl OverlordCrypto for HipCrypto {
     fn verify_aggregated_signature(&self, aggregated_signature: Bytes, hash: Bytes, voters: Vec<Bytes>) -> Result<(), Box<dyn Error + Send>> {
         let (v, vl) = concat(&voters);
         check(unsafe {
-            ffi::ovh_verify_aggregated(self.ctx.0, aggregated_signature.as_ptr(), aggregated_signature.len(),
+            ffi::ovh_verify_aggregated(self.raw(), aggregated_signature.as_ptr(), aggregated_signature.len(),
                                        hash.as_ptr(), hash.len(), v.as_ptr(), vl.as_ptr(), vl.len())
         })
     }

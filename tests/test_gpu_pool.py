@@ -78,3 +78,99 @@ def test_inputs_overwritten_on_ovh_stream_after_enqueue(votes):
     del src, d_s, d_h, d_p, junk, codes
     torch.cuda.synchronize()
     ctx.close()
+
+
+def _bad_jobs(votes):
+    s, h, p = votes
+    n = len(s)
+    bad_s, bad_p = s.copy(), p.copy()
+    for i in sv.seeded_positions(n, 0.01, 53):
+        bad_s[i] = np.frombuffer(sv.add_g2(bytes(bad_s[i])), dtype=np.uint8)
+    bad_p[11] = np.frombuffer(bytes.fromhex("ff" * 48), dtype=np.uint8)
+    return bad_s, bad_p, sv.oracle_codes(bad_s, h, bad_p)
+
+
+def test_pinned_host_inputs_on_ovh_stream_then_close(votes):
+    """The r05ab pattern: the inputs come from PINNED host tensors copied
+    with non_blocking=True on torch.cuda.ExternalStream(ctx.stream), so torch's pinned-host
+    allocator records its own events on the library's stream; the context is then closed while
+    those blocks are still cached and their events not yet queried. ovh_destroy parks its streams
+    instead of destroying them (include/ovhip.h), so the allocator's later event queries -- on
+    freeing the tensors, on the next pinned allocation, and in a second context that takes the
+    parked streams back -- touch live streams. Codes equal the oracle's."""
+    import torch
+    from consensus_overlord_amd import device as dev
+    from consensus_overlord_amd.crypto import Context
+    s, h, p = votes
+    n = len(s)
+    bad_s, bad_p, want_bad = _bad_jobs(votes)
+    jobs = [(s, p), (bad_s, bad_p), (s, p), (bad_s, bad_p)]
+    ctx = Context(0)
+    ovh = torch.cuda.ExternalStream(ctx.stream)
+    src = [(torch.from_numpy(a.copy()).pin_memory(), torch.from_numpy(b.copy()).pin_memory()) for a, b in jobs]
+    d_h = torch.from_numpy(h).cuda()
+    ins = [(torch.empty((n, 96), dtype=torch.uint8, device="cuda"),
+            torch.empty((n, 48), dtype=torch.uint8, device="cuda")) for _ in jobs]
+    codes = [torch.full((n,), -1, dtype=torch.int32, device="cuda") for _ in jobs]
+    torch.cuda.synchronize()
+    for k in range(len(jobs)):
+        with torch.cuda.stream(ovh):
+            ins[k][0].copy_(src[k][0], non_blocking=True)
+            ins[k][1].copy_(src[k][1], non_blocking=True)
+        dev.verify_batch_async(ctx, ins[k][0], d_h, ins[k][1], codes[k])
+    dev.batch_wait(ctx)
+    got = [c.cpu().numpy() for c in codes]
+    ctx.close()                      # streams parked; torch still holds events recorded on them
+    del src                          # the pinned blocks go back to torch's cache (event bookkeeping)
+    more = torch.empty((n, 96), dtype=torch.uint8).pin_memory()   # the allocator processes its events
+    ctx2 = Context(0)                # takes the parked streams back
+    ovh2 = torch.cuda.ExternalStream(ctx2.stream)
+    with torch.cuda.stream(ovh2):
+        more.copy_(torch.from_numpy(s), non_blocking=False)
+        ins[0][0].copy_(more, non_blocking=True)
+    c2 = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    dev.verify_batch_async(ctx2, ins[0][0], d_h, ins[0][1], c2)
+    dev.batch_wait(ctx2)
+    assert (c2.cpu().numpy() == 0).all()
+    ctx2.close()
+    del more, ins, codes, c2
+    torch.cuda.synchronize()
+    for k in range(len(jobs)):
+        if k % 2 == 0:
+            assert (got[k] == 0).all(), (k, np.nonzero(got[k])[0][:8])
+        else:
+            assert got[k].tolist() == want_bad.tolist(), k
+
+
+def test_async_batch_then_shard_partial_without_wait(votes):
+    """a pipelined batch (persistent pool grids) and, with no ovh_batch_wait
+    between them, a shard batch (ovh_batch_partial_device on a stream: a grid of its own on the
+    other pool stream) are in the pool together. Each pool stream has its own fixed spill-scratch
+    region, so no two co-resident workgroups share one; both batches' codes equal the oracle's."""
+    import torch
+    from consensus_overlord_amd import device as dev
+    from consensus_overlord_amd.crypto import Context
+    s, h, p = votes
+    n = len(s)
+    bad_s, bad_p, want_bad = _bad_jobs(votes)
+    ctx = Context(0)
+    d_h = torch.from_numpy(h).cuda()
+    a_s, a_p = torch.from_numpy(bad_s).cuda(), torch.from_numpy(bad_p).cuda()
+    b_s, b_p = torch.from_numpy(s).cuda(), torch.from_numpy(p).cuda()
+    codes_a = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    codes_b = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    codes_c = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    part = torch.zeros((1, 864), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        dev.verify_batch_async(ctx, a_s, d_h, a_p, codes_a)
+        dev.batch_partial(ctx, a_s, d_h, a_p, codes_b, part[0], stream=True)
+        dev.combine_partials_async(ctx, part, n, codes_b, stream=True)
+        dev.verify_batch_async(ctx, b_s, d_h, b_p, codes_c)
+    dev.batch_wait(ctx)
+    torch.cuda.synchronize()
+    assert codes_a.cpu().numpy().tolist() == want_bad.tolist()
+    assert codes_b.cpu().numpy().tolist() == want_bad.tolist()
+    assert (codes_c.cpu().numpy() == 0).all()
+    ctx.close()
