@@ -137,11 +137,16 @@ def cpu_baseline(sigs: np.ndarray, hs: np.ndarray, pks: np.ndarray, budget_s: fl
             model = next((ln.split(":", 1)[1].strip() for ln in fh if ln.startswith("model name")), None)
     except OSError:
         pass
+    mulx = bool(orc.load().orc_mulx_active())
     return {"value": round(len(sigs) / dt_b, 2), "unit": "verifications/s", "cores": threads, "kind": "port",
             "per_core": round(len(sigs) / dt_b / threads, 2),
+            # r06: the port's Montgomery product as BMI2 mulx + ADX adcx / adox
+            # asm (oracle/c/mont_mulx.h; 1.65x per core on the per-vote verify) at -O3
+            "fp_mul": "mulx/adx asm" if mulx else "portable u128 CIOS",
             "cpu_model": model, "host_cpus": os.cpu_count(), "allowance": cpu_info,
             "sample": "all %d votes of the workload, RLC batch verify on %d threads = every CPU this job may "
-                      "run on (C restatement oracle/c/bls_oracle.c, not blst), %.2f s" % (len(sigs), threads, dt_b),
+                      "run on (C restatement oracle/c/bls_oracle.c, %s product, not blst), %.2f s" % (
+                          len(sigs), threads, "mulx/adx" if mulx else "portable", dt_b),
             "serial_1core": {"value": round(n1 / dt_1, 2), "cores": 1,
                              "sample": "first %d votes, per-vote verify_signature serially (the reference's "
                                        "call shape), %.2f s" % (n1, dt_1)}}

@@ -111,11 +111,33 @@ VM_FN void ld_slots4(Fp& A, Fp& B, Fp& C, Fp& D, const uint32_t* __restrict__ sl
   unpack4(B, 2, b2); unpack4(D, 2, d2); unpack4(A, 2, a2); unpack4(C, 2, c2);
   return;
 #endif
+#if defined(__HIP_DEVICE_COMPILE__)
+  // LDS byte addresses (r06): bit 11 of a reference selects the constant table through a
+  // sign-extended bit-field extract used as a bit-select mask (v_bfe_i32 + v_bfi_b32, where r05's
+  // pointer select took and / compare / cndmask), the low 11 bits index 48-byte entries
+  // (v_bfe_u32 + v_mad_u32_u24)
+  // (the select is written as v_bfi_b32 in asm: as C the compiler turns it back into the VCC
+  // compare + cndmask, whose VCC write-then-read also costs wait states)
+  typedef const __attribute__((address_space(3))) u32x4* lds_q;
+  const uint32_t sb = (uint32_t)(uintptr_t)(lds_cptr)slots, cb = (uint32_t)(uintptr_t)(lds_cptr)cst;
+  auto addr = [&](uint32_t ref) -> lds_q {
+    const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ref, 11, 1);
+    uint32_t base;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(base) : "v"(m), "v"(cb), "v"(sb));
+    return (lds_q)(uintptr_t)(__builtin_amdgcn_ubfe(ref, 0, 11) * 48u + base);
+  };
+  const lds_q pa = addr(ra), pb = addr(rb), pc = addr(rc), pd = addr(rd);
+#else
   const uint4 *pa = slot_ptr(slots, cst, ra), *pb = slot_ptr(slots, cst, rb), *pc = slot_ptr(slots, cst, rc),
               *pd = slot_ptr(slots, cst, rd);
+#endif
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const u32x4 b = pb[q], d = pd[q], a = pa[q], c = pc[q];
+#else
     const uint4 b = pb[q], d = pd[q], a = pa[q], c = pc[q];
+#endif
     B.v[4 * q] = b.x; B.v[4 * q + 1] = b.y; B.v[4 * q + 2] = b.z; B.v[4 * q + 3] = b.w;
     D.v[4 * q] = d.x; D.v[4 * q + 1] = d.y; D.v[4 * q + 2] = d.z; D.v[4 * q + 3] = d.w;
     A.v[4 * q] = a.x; A.v[4 * q + 1] = a.y; A.v[4 * q + 2] = a.z; A.v[4 * q + 3] = a.w;
@@ -227,26 +249,24 @@ VM_FN void lin_mad(Fp& r, const Fp& A, const Fp& B, const Fp& C, const Fp& D, in
   }
 }
 
-// Product operands x = A + (nx ? 2p - B : B), y = C + (ny ? 2p - D : D) in [0, 4p), no
-// reduction. The negations' borrow chains run only when some lane of the wave has one
-// (`any_neg`); both paths write x, y in full (no register copies at the join). The four carry
-// chains are skewed by one limb so no chain reads its carry right after writing it (gfx950
-// wait states).
-VM_FN void pre_add2(Fp& x, const Fp& A, const Fp& B, bool nx, Fp& y, const Fp& C, const Fp& D, bool ny,
-                    bool any_neg) {
+// Product operands x = A + B, y = C + (ny ? 2p - D : D) in [0, 4p), no reduction. Only y is
+// ever negated: the encoder puts a product's negated operand on y (tools/fpvm/sched.py
+// lane_operands; no program negates both), so the negation's borrow chain runs once, and only
+// when some lane of the wave has one (`any_neg`, r06: 77 -> 53 VALU in the 1,062 of the vote
+// program's 1,375 product phases that have one). Both paths write x, y in full (no register
+// copies at the join). The carry chains are skewed by one limb so no chain reads its carry
+// right after writing it (gfx950 wait states).
+VM_FN void pre_add2(Fp& x, const Fp& A, const Fp& B, Fp& y, const Fp& C, const Fp& D, bool ny, bool any_neg) {
   uint32_t c1 = 0, c2 = 0;
   if (any_neg) {
-    uint32_t nb[12], nd[12], b1 = 0, b2 = 0;
+    uint32_t nd[12], b2 = 0;
 #pragma unroll
     for (int j = 0; j < 13; ++j) {
       if (j < 12) {
-        nb[j] = subc32(P2_LIMBS[j], B.v[j], b1, &b1);
         nd[j] = subc32(P2_LIMBS[j], D.v[j], b2, &b2);
+        x.v[j] = addc32(A.v[j], B.v[j], c1, &c1);
       }
-      if (j >= 1) {
-        x.v[j - 1] = addc32(A.v[j - 1], nx ? nb[j - 1] : B.v[j - 1], c1, &c1);
-        y.v[j - 1] = addc32(C.v[j - 1], ny ? nd[j - 1] : D.v[j - 1], c2, &c2);
-      }
+      if (j >= 1) y.v[j - 1] = addc32(C.v[j - 1], ny ? nd[j - 1] : D.v[j - 1], c2, &c2);
     }
   } else {
 #pragma unroll
@@ -257,22 +277,22 @@ VM_FN void pre_add2(Fp& x, const Fp& A, const Fp& B, bool nx, Fp& y, const Fp& C
   }
 }
 
-// s = sa A + sb B + sc C + sd D with unit signs (a zero coefficient points its operand at the
-// zero constant), s < 8p in 12 limbs: a negated term enters as ~X and the offset K = n (2p + 1)
-// (n negated terms, constant-table entry KTAB + n) turns each ~X into 2p - X modulo 2^384.
-// Four carry chains (A' + B', C' + D', their sum, + K) skewed by one limb each.
-VM_FN void lin_sum(uint32_t* s, const Fp& A, const Fp& B, const Fp& C, const Fp& D, int sa, int sb, int sc,
-                   int sd, bool any_neg, const uint32_t* __restrict__ cst) {
+// s = A + sb B + sc C + sd D with unit signs (a zero coefficient points its operand at the zero
+// constant), s < 8p in 12 limbs: a negated term enters as ~X (mb, mc, md: all-ones masks of the
+// negated terms; a unit sum's first term is never negated, ir._expand_unit) and the offset
+// K = n (2p + 1) (n negated terms, constant-table entry KTAB + n) turns each ~X into 2p - X
+// modulo 2^384. Four carry chains (A + B', C' + D', their sum, + K) skewed by one limb each.
+VM_FN void lin_sum(uint32_t* s, const Fp& A, const Fp& B, const Fp& C, const Fp& D, uint32_t mb, uint32_t mc,
+                   uint32_t md, bool any_neg, const uint32_t* __restrict__ cst) {
   uint32_t u[12], v[12], w[12], c1 = 0, c2 = 0, c3 = 0, c4 = 0;
   if (any_neg) {
-    const uint32_t ma = sa < 0 ? ~0u : 0u, mb = sb < 0 ? ~0u : 0u, mc = sc < 0 ? ~0u : 0u, md = sd < 0 ? ~0u : 0u;
-    const uint32_t n = (ma & 1u) + (mb & 1u) + (mc & 1u) + (md & 1u);
+    const uint32_t n = (mb & 1u) + (mc & 1u) + (md & 1u);
     Fp K;
     ld_slot(K, nullptr, cst, CONST_BASE + KTAB + n);
 #pragma unroll
     for (int j = 0; j < 14; ++j) {
       if (j < 12) {
-        u[j] = addc32(A.v[j] ^ ma, B.v[j] ^ mb, c1, &c1);
+        u[j] = addc32(A.v[j], B.v[j] ^ mb, c1, &c1);
         v[j] = addc32(C.v[j] ^ mc, D.v[j] ^ md, c2, &c2);
       }
       if (j >= 1 && j <= 12) w[j - 1] = addc32(u[j - 1], v[j - 1], c3, &c3);
@@ -317,47 +337,52 @@ inline uint32_t uniform(uint32_t w0) { return w0; }
 //   linear    lin_mad: k (A + cb B + cc C + cd D) with unit signs, or general coefficients
 //             |c| <= 15, and selb (bit imm of the vote's scalar ? C : B);
 //   rare      sel, logic, st, inv (per-lane branches).
+// The sign of the 5-bit two's-complement coefficient field whose top bit is `bit` of w3, as a
+// mask (a bit-field extract on the device)
+VM_FN uint32_t sign_mask(uint32_t w, int bit) { return (uint32_t)((int32_t)(w << (31 - bit)) >> 31); }
+VM_FN int coef5(uint32_t w, int lo) { return ((int)(w << (27 - lo))) >> 27; }
+
+// r06: only what every phase needs is decoded up front (the header, the opcode, the four operand
+// addresses); each block extracts its own fields (dst, coefficient signs, scale, imm), so a
+// product phase no longer pays for the linear blocks' decoding (r05: 10 VALU per phase).
 VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
                 uint64_t scalar, const Out& out) {
-  const uint32_t op = active ? (in.x & 31) : (uint32_t)OP_NOP;
   // the phase header (bits 22.. of w0, equal in every lane; tools/fpvm/sched.py phase_bits) names
   // the blocks some lane of the phase needs: scalar branches, no ballots
   const uint32_t hdr = uniform(in.x);
   if (!(hdr & H_ANY)) return;
-  const uint32_t dst = (in.x >> 5) & 0x7FF;
-  const uint32_t imm = (in.x >> 16) & 63;
+  const uint32_t op = active ? (in.x & 31) : (uint32_t)OP_NOP;
   // four operands, always valid references (a missing one is the zero constant); selb (bit imm
   // of the vote's scalar ? C : B) is a one-term unit lin: A := the picked operand, B = C = 0
+  // (its encoded coefficients and scale are 0: tools/fpvm/sched.py lane_operands)
   uint32_t ra = in.y & 0xFFFF, rb = in.y >> 16, rc = in.z & 0xFFFF;
-  int ca = ((int)(in.w << 27)) >> 27, cb = ((int)(in.w << 22)) >> 27;
-  int cc = ((int)(in.w << 17)) >> 27, cd = ((int)(in.w << 12)) >> 27;
   bool selb = false;
   if (hdr & H_SELB) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // (kept a branch: if-converted, these selects ran in every phase, r06 ISA)
+    __asm__ volatile("");
+#endif
     selb = op == OP_SELB;
-    const bool bit = ((scalar >> imm) & 1) != 0;
+    const bool bit = ((scalar >> ((in.x >> 16) & 63)) & 1) != 0;
     ra = selb ? (bit ? rc : rb) : ra;
     rb = selb ? CONST_BASE + KZERO : rb;
     rc = selb ? CONST_BASE + KZERO : rc;
-    ca = selb ? 1 : ca;
-    cb = selb ? 0 : cb;
-    cc = selb ? 0 : cc;
-    cd = selb ? 0 : cd;
   }
   Fp A, B, C, D;
   ld_slots4(A, B, C, D, slots, cst, ra, rb, rc, in.z >> 16);
-  const bool is_mul = op == OP_MULS || op == OP_SGN0 || op == OP_LEX || op == OP_EQ;
-  // unit sums run the add-chain block unless the encoder forced the general block (a linear
-  // phase runs one block: tools/fpvm/sched.py PHASE_UNIT, FORCE_ACC = w3 bit 24)
-  const bool lin_unit = !(in.w & (1u << 24)) && ca == 1 && cb >= -1 && cb <= 1 && cc >= -1 && cc <= 1 && cd >= -1 &&
-                        cd <= 1;
-  const bool is_lin = (op == OP_LIN && lin_unit) || selb;
-  const bool is_acc = op == OP_LIN && !lin_unit;
+  const uint32_t dst = (in.x >> 5) & 0x7FF;
+  // A phase's lin ops all run in one block (tools/fpvm/sched.py encode, PHASE_UNIT, asserted):
+  // the unit-sum block, or every lin op in the general block with FORCE_ACC (w3 bit 24) set. So
+  // a lane's block is that bit (r05 re-derived it from the coefficients in every phase); selb
+  // ops run in the unit block
+  const bool force_acc = (in.w & (1u << 24)) != 0;
   if (hdr & H_MUL) {
+    const bool is_mul = op == OP_MULS || op == OP_SGN0 || op == OP_LEX || op == OP_EQ;
     Fp x, y, m;
-    pre_add2(x, A, B, cb < 0, y, C, D, cd < 0, (hdr & H_MULNEG) != 0);
+    pre_add2(x, A, B, y, C, D, sign_mask(in.w, 19) != 0, (hdr & H_MULNEG) != 0);
     fp_mul(m, x, y);
-    const bool flag = is_mul && op != OP_MULS;
-    if (hdr & H_FLAG) {  // m is canonical here: y = 1, x < 4p -> x / 2^384 + p rounds to <= p
+    if (hdr & H_FLAG) {  // m is canonical here: the product of a value below 4p and the plain 1
+      const bool flag = is_mul && op != OP_MULS;
       uint32_t f = 0;
       if (op == OP_SGN0) f = m.v[0] & 1u;
       if (op == OP_LEX) f = limbs_gt(m.v, HALF_P) ? 1u : 0u;
@@ -369,20 +394,23 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
   }
   if (hdr & H_LIN) {
     uint32_t s[13];
-    lin_sum(s, A, B, C, D, 1, cb, cc, cd, (hdr & H_LINNEG) != 0, cst);
-    // "scaled" form k * (unit sum), k < 16 (k <= 1: unchanged)
-    const uint32_t k = selb ? 1u : (in.w >> 20) & 15;
+    lin_sum(s, A, B, C, D, sign_mask(in.w, 9), sign_mask(in.w, 14), sign_mask(in.w, 19), (hdr & H_LINNEG) != 0,
+            cst);
+    // "scaled" form k * (unit sum), k < 16 (k <= 1: unchanged; selb: 0)
+    const uint32_t k = (in.w >> 20) & 15;
     Fp l;
     scale_reduce(l, s, k > 1 ? k : 1u);
-    if (is_lin) st_slot(slots, dst, l);
+    if ((op == OP_LIN && !force_acc) || selb) st_slot(slots, dst, l);
   }
   if (hdr & H_ACC) {  // general coefficients
     Fp l;
-    lin_mad(l, A, B, C, D, ca, cb, cc, cd);
-    if (is_acc) st_slot(slots, dst, l);
+    lin_mad(l, A, B, C, D, coef5(in.w, 0), coef5(in.w, 5), coef5(in.w, 10), coef5(in.w, 15));
+    if (op == OP_LIN && force_acc) st_slot(slots, dst, l);
   }
-  const bool rare = op != OP_NOP && !is_mul && !is_lin && !is_acc;
   if (hdr & H_RARE) {
+    const bool rare = op != OP_NOP && op != OP_LIN && !selb && op != OP_MULS && op != OP_SGN0 && op != OP_LEX &&
+                      op != OP_EQ;
+    const uint32_t imm = (in.x >> 16) & 63;
     Fp z = A;
     if (op == OP_ST) {
       canon(z, A);
@@ -402,6 +430,15 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
     }
     if (rare && op != OP_ST) st_slot(slots, dst, z);
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  // Every path of the phase retires its operand reads here (free on the paths that consumed
+  // them). Left pending on some path, they merged into the loop head's wait-count state, and
+  // the next phase's first write of a register one of them had loaded (an operand address) got
+  // an lgkmcnt(0): a wait for this phase's result stores before the next phase could issue its
+  // reads (r06 ISA). LDS operations complete in order, so the last quarter of each operand
+  // covers all twelve reads.
+  __asm__ volatile("" ::"v"(A.v[11]), "v"(B.v[11]), "v"(C.v[11]), "v"(D.v[11]));
+#endif
 }
 
 // Run `nphases` phases of a W-lane program (the code is phase-major: lane l of phase t at
@@ -438,25 +475,27 @@ __device__ __forceinline__ void run(const uint4* __restrict__ code, uint32_t nph
                                     bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
                                     uint64_t scalar, const Out& out, uint64_t* __restrict__ trace = nullptr,
                                     const uint32_t* __restrict__ side = nullptr, uint32_t* __restrict__ scr = nullptr) {
-  static_assert(PREFETCH == 4, "prefetch ring below is 4 deep");
+  static_assert(PREFETCH >= 2, "the code and side words carry PREFETCH trailing phases");
   if constexpr (SIDE) {
-    uint4 q0 = code[lane], q1 = code[(size_t)W + lane], q2 = code[(size_t)2 * W + lane],
-          q3 = code[(size_t)3 * W + lane];
-    uint32_t s0 = side[lane], s1 = side[W + lane], s2 = side[2 * W + lane], s3 = side[3 * W + lane];
+    // r06: instruction words one phase ahead and side words two (a fill's load is issued in the
+    // phase before its own), a ring of one / two registers: r05's four-deep rings cost a 12-VALU
+    // rotation in every phase, and the rotation's copy of the newest load waited for it at the
+    // end of the phase anyway (s_waitcnt vmcnt(0) before the moves)
+    uint4 q = code[lane];
+    uint32_t s0 = side[lane], s1 = side[W + lane];
     // inactive lanes (a slice past the batch's end) run no side op: their unit has no scratch
-    if (!active) s0 = s1 = s2 = s3 = 0;
+    if (!active) s0 = s1 = 0;
+    // the first words complete before the loop: the compiler loads them straight into the loop's
+    // registers, and its wait-count state merged at the loop head then made every phase wait for
+    // its own fresh prefetch (vmcnt(0) before the header's readfirstlane, r06 ISA)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #pragma unroll 1
     for (uint32_t ph = 0; ph < nphases; ++ph) {
-      const uint4 cur = q0;
-      q0 = q1;
-      q1 = q2;
-      q2 = q3;
-      q3 = code[(size_t)(ph + PREFETCH) * W + lane];
+      const uint4 cur = q;
+      q = code[(size_t)(ph + 1) * W + lane];
       const uint32_t sw = s0;
       s0 = s1;
-      s1 = s2;
-      s2 = s3;
-      s3 = active ? side[(size_t)(ph + PREFETCH) * W + lane] : 0u;
+      s1 = active ? side[(size_t)(ph + 2) * W + lane] : 0u;
       // the fill of phase ph + 1 (its side word is s0 now): issue the load before this phase
       const bool fill = (s0 & (SIDE_VALID | SIDE_FILL)) == (SIDE_VALID | SIDE_FILL);
       u32x4 f0, f1, f2;

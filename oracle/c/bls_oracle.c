@@ -84,8 +84,8 @@ static void fp_sub(fp* r, const fp* a, const fp* b) {
   memcpy(r->l, t, 48);
 }
 
-/* CIOS Montgomery product a b R^-1 mod p */
-static void fp_mul(fp* r, const fp* a, const fp* b) {
+/* CIOS Montgomery product a b R^-1 mod p (portable; the reference for the mulx form below) */
+static void fp_mul_cios(fp* r, const fp* a, const fp* b) {
   uint64_t t[8] = {0};
   for (int i = 0; i < 6; ++i) {
     uint64_t c = 0;
@@ -111,6 +111,26 @@ static void fp_mul(fp* r, const fp* a, const fp* b) {
   }
   if (t[6] || limbs_geq_p(t)) sub_p(t);
   memcpy(r->l, t, 48);
+}
+
+#if defined(__x86_64__)
+#include "mont_mulx.h"
+#endif
+/* 1: the product runs as BMI2 mulx + ADX adcx / adox asm (tools/gen_mulx.py; chosen at init by
+ * CPUID unless ORC_NO_MULX is set), 0: the portable CIOS. The two agree bit for bit
+ * (orc_mulx_selftest, tests/test_oracle_c.py); only the timed CPU baseline cares which runs. */
+static int g_mulx = 0;
+
+static void fp_mul(fp* r, const fp* a, const fp* b) {
+#if defined(__x86_64__)
+  /* (the asm form assumes canonical operands, t < 2^447 in seven limbs; hash_to_field multiplies
+   * raw 384-bit halves, which take the CIOS) */
+  if (g_mulx && a->l[5] < P[5] && b->l[5] < P[5]) {
+    fp_mul_mulx(r->l, a->l, b->l, P, PINV);
+    return;
+  }
+#endif
+  fp_mul_cios(r, a, b);
 }
 
 static void fp_sqr(fp* r, const fp* a) { fp_mul(r, a, a); }
@@ -1104,6 +1124,12 @@ static void init_once(void) {
   uint64_t inv = 1;
   for (int i = 0; i < 7; ++i) inv *= 2 - P[0] * inv;
   PINV = (uint64_t)0 - inv;
+#if defined(__x86_64__)
+  {
+    const char* off = getenv("ORC_NO_MULX");
+    g_mulx = __builtin_cpu_supports("bmi2") && __builtin_cpu_supports("adx") && !(off && *off && *off != '0');
+  }
+#endif
   /* R mod p, R^2, R^3 by doubling (plain arithmetic on limbs) */
   uint64_t v[6] = {1, 0, 0, 0, 0, 0};
   for (int k = 0; k < 384 * 2; ++k) {
@@ -1222,6 +1248,46 @@ static void init(void) { pthread_once(&ONCE, init_once); }
 static const uint8_t DEFAULT_DST[] = "BLS_SIG_BLS12381G2_XMD:SHA-256_SSWU_RO_NUL_";
 static const uint8_t* g_dst = DEFAULT_DST;
 static size_t g_dst_len = 43;
+
+/* Which Montgomery product the oracle runs (1: mulx / ADX asm, 0: portable CIOS). */
+int orc_mulx_active(void) {
+  init();
+  return g_mulx;
+}
+
+/* The mulx product against the portable CIOS on n pseudo-random canonical operand pairs (and
+ * the edge values 0, 1, p - 1): the number of mismatches (0 when the mulx form is unavailable). */
+int orc_mulx_selftest(uint64_t seed, int n) {
+  init();
+  int bad = 0;
+#if defined(__x86_64__)
+  if (!(__builtin_cpu_supports("bmi2") && __builtin_cpu_supports("adx"))) return 0;
+  uint64_t x = seed | 1;
+  for (int k = 0; k < n + 9; ++k) {
+    fp a, b, r1, r2;
+    for (int h = 0; h < 2; ++h) {
+      fp* t = h ? &b : &a;
+      const int e = k < 9 ? (h ? k % 3 : k / 3) : -1;
+      if (e >= 0) { /* 0, 1, p - 1 */
+        memset(t->l, 0, 48);
+        if (e == 1) t->l[0] = 1;
+        if (e == 2) { memcpy(t->l, P, 48); t->l[0] -= 1; }
+        continue;
+      }
+      for (int i = 0; i < 6; ++i) {
+        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+        t->l[i] = x;
+      }
+      t->l[5] &= (1ull << 61) - 1;
+      while (limbs_geq_p(t->l)) sub_p(t->l);
+    }
+    fp_mul_cios(&r1, &a, &b);
+    fp_mul_mulx(r2.l, a.l, b.l, P, PINV);
+    bad += memcmp(r1.l, r2.l, 48) != 0;
+  }
+#endif
+  return bad;
+}
 
 void orc_set_dst(const uint8_t* dst, size_t len) {
   static uint8_t buf[256];

@@ -43,6 +43,8 @@ def load(build_if_missing: bool = True):
                                              _vp]),
         "orc_sk_keygen": (ctypes.c_int, [_u8, _sz, _u8]),
         "orc_combine_partials": (ctypes.c_int, [_sz, _vp, ctypes.POINTER(ctypes.c_int)]),
+        "orc_mulx_active": (ctypes.c_int, []),
+        "orc_mulx_selftest": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int]),
         "orc_batch_fallback": (ctypes.c_int, [_sz, _vp, _vp, _vp, _vp, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():

@@ -103,3 +103,12 @@ def test_batch_rlc_matches_per_vote(golden, threads):
     good = [i for i, c in enumerate(cases) if c["code"] == 0]
     codes, ok = orc.verify_batch_rlc(sigs[good], hs[good], pks[good], seed=6, threads=threads)
     assert ok and (codes == 0).all()
+
+
+def test_mulx_product_matches_portable_cios():
+    """the oracle's Montgomery product runs as BMI2 mulx + ADX adcx / adox asm
+    (oracle/c/mont_mulx.h, tools/gen_mulx.py) when the CPU has them -- only to make the timed CPU
+    baseline closer to what blst would do. It must agree with the portable u128 CIOS bit for bit:
+    200,000 random canonical operand pairs plus the edge values 0, 1, p - 1, and (the golden
+    tests above) every verdict and byte the oracle produces."""
+    assert orc.load().orc_mulx_selftest(0xC17A, 200000) == 0

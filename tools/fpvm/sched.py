@@ -30,6 +30,8 @@ OPC = {"nop": 0, "muls": 1, "sgn0": 2, "lex": 3, "inv": 4, "lin": 5, "sel": 6, "
        "xor": 10, "st": 11, "selb": 12, "sop": 13, "spill": 14, "fill": 15}
 CONST_BASE = 0x800
 ABSENT = 0xFFFF
+# ops the interpreter runs through the Montgomery product (x = A + cb B, y = C + cd D)
+PRODUCTS = ("muls", "sgn0", "lex", "eq")
 # LDS pass width (lanes) and slot residues that share banks (OVH_BANK="lanes,mod" for A/B builds)
 BANK_LANES, BANK_MOD = (int(x) for x in os.environ.get("OVH_BANK", "16,16").split(","))
 # passes of the bank-conflict local search over the slot assignment (improve_banks; 0 = off)
@@ -463,6 +465,12 @@ def lane_operands(prog, i, unit=False):
             else:
                 C, D = u[0][1], u[1][1]
             coefs[h], coefs[h + 1] = u[0][0], u[1][0]
+        if coefs[1] < 0:
+            # r06: the negated operand on y = C + cd D (fpvm.hpp pre_add2 has no x negation
+            # chain); x y is symmetric and both operands stay below 4p. No program negates both
+            assert coefs[3] >= 0, ("%s: both product operands negated" % prog.name, op.coefs)
+            A, B, C, D = C, D, A, B
+            coefs[:4] = [coefs[2], coefs[3], coefs[0], coefs[1]]
     elif k == "sop":           # A C + cb B D
         A, B, C, D = s[:4]
         coefs[:4] = list(op.coefs[:4])
@@ -530,15 +538,30 @@ def encode(sc):
                 cref = sc.consts.ref(R_MONT * R_MONT % P, False)   # raw R^3: back to Montgomery
             else:
                 cref = _operand(sc, C)
+            xa, xb = _operand(sc, A), _operand(sc, B)
+            if k in PRODUCTS and coefs[1] < 0:
+                # r06: a product's negated operand always on y = C + cd D (fpvm.hpp pre_add2 has
+                # no x negation chain; lane_operands swaps muls operands already): eq's x = A - B
+                # goes to y, and x = the plain 1 (x y is symmetric)
+                assert k == "eq" and coefs[3] >= 0, ("%s: x operand negated" % sc.prog.name, k, coefs)
+                xa, xb, cref, dref = cref, _operand(sc, D), xa, xb
+                coefs = [coefs[2], coefs[3], coefs[0], coefs[1]] + coefs[4:]
+            else:
+                dref = _operand(sc, D)
             w3 = _c5(coefs[0]) | _c5(coefs[1]) << 5 | _c5(coefs[2]) << 10 | _c5(coefs[3]) << 15 | scale << 20
             if k == "lin" and not unit and ALL_ACC:
                 w3 |= FORCE_ACC
-            words += [w0, _operand(sc, A) | _operand(sc, B) << 16, cref | _operand(sc, D) << 16, w3]
+            words += [w0, xa | xb << 16, cref | dref << 16, w3]
         # the phase header (wave-uniform code paths) in bits 22.. of every lane's w0
         base = len(words) - sc.W * nw
         hdr = 0
-        for lane in range(sc.W):
-            hdr |= phase_bits(words[base + lane * nw:base + lane * nw + 4])
+        lane_bits = [phase_bits(words[base + lane * nw:base + lane * nw + 4]) for lane in range(sc.W)]
+        for b in lane_bits:
+            hdr |= b
+        # fpvm.hpp exec picks a lin lane's block from the header alone (H_ACC: every lin op of the
+        # phase in the general block): no phase may mix unit-block and general-block lin ops
+        if hdr & H_ACC:
+            assert not any(b & H_LIN and not b & H_SELB for b in lane_bits), (sc.prog.name, "mixed lin blocks")
         for lane in range(sc.W):
             words[base + lane * nw] |= hdr
     return words
@@ -629,14 +652,16 @@ def simulate(sc, words, inputs: dict, scalar: int = 0):
             else:
                 x = (ca * A + cb * B) % P
                 y = (cc * C + cd * D) % P
+                # the flag ops read the from-Montgomery product x y of a value and the plain 1
+                # (either operand: encode() moves eq's A - B to y)
                 if opc == OPC["muls"]:
                     z = x * y % P
                 elif opc == OPC["sgn0"]:
-                    z = x & 1
+                    z = x * y % P & 1
                 elif opc == OPC["lex"]:
-                    z = 1 if x > HALF_P else 0
+                    z = 1 if x * y % P > HALF_P else 0
                 elif opc == OPC["eq"]:
-                    z = 1 if x == 0 else 0
+                    z = 1 if x * y % P == 0 else 0
                 else:
                     raise ValueError(opc)
             results.append((dst, z))
