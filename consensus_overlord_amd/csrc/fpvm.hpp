@@ -37,8 +37,9 @@ enum : uint32_t {
   OP_AND = 8, OP_OR = 9, OP_XOR = 10, OP_ST = 11, OP_SELB = 12,
 };
 
-// phases of instruction prefetch (the uploaded code carries this many trailing NOP phases)
-constexpr uint32_t PREFETCH = 4;
+// trailing NOP phases the uploaded code and side words carry (run's unrolled loops read past the
+// end; r05's prefetch distance)
+constexpr uint32_t PREFETCH = 6;
 
 // Where `st` ops write: plane `imm` of unit `unit` in a structure-of-arrays slab (limb k of
 // plane j at base[(j * 12 + k) * cap + unit]).
@@ -475,68 +476,76 @@ __device__ __forceinline__ void run(const uint4* __restrict__ code, uint32_t nph
                                     bool active, uint32_t* __restrict__ slots, const uint32_t* __restrict__ cst,
                                     uint64_t scalar, const Out& out, uint64_t* __restrict__ trace = nullptr,
                                     const uint32_t* __restrict__ side = nullptr, uint32_t* __restrict__ scr = nullptr) {
-  static_assert(PREFETCH >= 2, "the code and side words carry PREFETCH trailing phases");
+  static_assert(PREFETCH >= 5, "the unrolled loops below read up to 4 phases past the end");
   if constexpr (SIDE) {
-    // r06: instruction words one phase ahead and side words two (a fill's load is issued in the
-    // phase before its own), a ring of one / two registers: r05's four-deep rings cost a 12-VALU
-    // rotation in every phase, and the rotation's copy of the newest load waited for it at the
-    // end of the phase anyway (s_waitcnt vmcnt(0) before the moves)
-    uint4 q = code[lane];
-    uint32_t s0 = side[lane], s1 = side[W + lane];
+    // r06: the loop is unrolled three times over three-register rings. At the start of phase ph
+    // the words of phase ph + 2 load into the registers that held phase ph - 1's (no register
+    // copies: r05's four-deep rings rotated 12 VALU per phase, and the copy of the newest load
+    // waited for it inside the same phase). The loads of a phase are issued at its start (the
+    // next phase's fill first), so whatever the compiler waits for at the next phase's start has
+    // had a whole phase. A partial last round runs up to two of the code's trailing NOP phases
+    // (no ops, zero side words).
+    uint4 qa = code[lane], qb = code[W + lane], qc;
+    uint32_t sa = side[lane], sb = side[W + lane], sc;
     // inactive lanes (a slice past the batch's end) run no side op: their unit has no scratch
-    if (!active) s0 = s1 = 0;
+    if (!active) sa = sb = 0;
     // the first words complete before the loop: the compiler loads them straight into the loop's
     // registers, and its wait-count state merged at the loop head then made every phase wait for
-    // its own fresh prefetch (vmcnt(0) before the header's readfirstlane, r06 ISA)
+    // its own fresh prefetch (r06 ISA)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#pragma unroll 1
-    for (uint32_t ph = 0; ph < nphases; ++ph) {
-      const uint4 cur = q;
-      q = code[(size_t)(ph + 1) * W + lane];
-      const uint32_t sw = s0;
-      s0 = s1;
-      s1 = active ? side[(size_t)(ph + 2) * W + lane] : 0u;
-      // the fill of phase ph + 1 (its side word is s0 now): issue the load before this phase
-      const bool fill = (s0 & (SIDE_VALID | SIDE_FILL)) == (SIDE_VALID | SIDE_FILL);
+    // phase ph: instruction q, side word s, the next phase's side word sn (its fill is issued
+    // now); q2 / s2 take phase ph + 2's words
+    auto step = [&](const uint4& q, uint4& q2, const uint32_t s, const uint32_t sn, uint32_t& s2,
+                    const uint32_t ph) __attribute__((always_inline)) {
+      const bool fill = (sn & (SIDE_VALID | SIDE_FILL)) == (SIDE_VALID | SIDE_FILL);
       u32x4 f0, f1, f2;
       if (fill) {
-        const u32x4* src = reinterpret_cast<const u32x4*>(scr + ((s0 >> 11) & 0xFFF) * 12);
+        const u32x4* src = reinterpret_cast<const u32x4*>(scr + ((sn >> 11) & 0xFFF) * 12);
         f0 = __builtin_nontemporal_load(src);
         f1 = __builtin_nontemporal_load(src + 1);
         f2 = __builtin_nontemporal_load(src + 2);
       }
-      exec(cur, active, slots, cst, scalar, out);
+      q2 = code[(size_t)(ph + 2) * W + lane];
+      s2 = active ? side[(size_t)(ph + 2) * W + lane] : 0u;
+      exec(q, active, slots, cst, scalar, out);
       // this phase's spill reads its slot before the fill lands: a fill may take the slot of a
       // value whose last read is this spill
-      side_spill(sw, slots, scr);
+      side_spill(s, slots, scr);
       if (fill) {
-        u32x4* d = reinterpret_cast<u32x4*>(slots + (s0 & 0x7FF) * 12);
+        u32x4* d = reinterpret_cast<u32x4*>(slots + (sn & 0x7FF) * 12);
         d[0] = f0;
         d[1] = f1;
         d[2] = f2;
       }
+    };
+#pragma unroll 1
+    for (uint32_t ph = 0; ph < nphases; ph += 3) {
+      step(qa, qc, sa, sb, sc, ph);
+      step(qb, qa, sb, sc, sa, ph + 1);
+      step(qc, qb, sc, sa, sb, ph + 2);
     }
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     return;
   }
   // trace (diagnostics, OVH_FLAG_VM_TRACE): wall clock after every phase
   if (trace && threadIdx.x == 0) trace[0] = wall_clock64();
-  // instructions are prefetched PREFETCH phases ahead (an HBM / L2 round trip outlasts a light
-  // phase); the code carries PREFETCH trailing NOP phases
-  uint4 q0 = code[lane], q1 = code[(size_t)W + lane], q2 = code[(size_t)2 * W + lane],
-        q3 = code[(size_t)3 * W + lane];
-#pragma unroll 1
-  for (uint32_t ph = 0; ph < nphases; ++ph) {
-    const uint4 cur = q0;
-    q0 = q1;
-    q1 = q2;
-    q2 = q3;
-    q3 = code[(size_t)(ph + PREFETCH) * W + lane];
-    exec(cur, active, slots, cst, scalar, out);
-    if (trace) {
+  // unrolled three times over a three-register ring, phase ph + 2's words loaded at the start of
+  // phase ph (as the side-word loop above); a partial last round runs trailing NOP phases
+  uint4 qa = code[lane], qb = code[W + lane], qc;
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), as above
+  auto step = [&](const uint4& q, uint4& q2, const uint32_t ph) __attribute__((always_inline)) {
+    q2 = code[(size_t)(ph + 2) * W + lane];
+    exec(q, active, slots, cst, scalar, out);
+    if (trace && ph < nphases) {
       __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (threadIdx.x == 0) trace[ph + 1] = wall_clock64();
     }
+  };
+#pragma unroll 1
+  for (uint32_t ph = 0; ph < nphases; ph += 3) {
+    step(qa, qc, ph);
+    step(qb, qa, ph + 1);
+    step(qc, qb, ph + 2);
   }
   // the caller reads results through LDS (other lanes' slots) and may reuse it
   __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
