@@ -45,6 +45,7 @@ G2_GEN_COMPRESSED = bytes.fromhex(
 R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 OVH_FLAG_PROFILE = 0x2
 OVH_FLAG_VM_CLOCK = 0x20
+OVH_FLAG_POOL_RESERVE = 0x40
 # Roofline denominators (integer VALU):
 #  PEAK_FULLRATE  the theoretical full-rate 32-bit VALU lane rate, 256 CU x 64 lanes/clk x
 #                 2.4 GHz = 3.93e13 lane-ops/s (one wave instruction per 4 cycles per SIMD)
@@ -488,6 +489,9 @@ def main():
                          "region; vote_spans then absent and the roofline uses the profile batches' stage time)")
     ap.add_argument("--shard-path", action="store_true",
                     help="diagnostic: run the multi-GPU pipeline (partials + RCCL all-gather) even at N=1")
+    ap.add_argument("--pool-reserve", action="store_true",
+                    help="A/B: contexts with OVH_FLAG_POOL_RESERVE (the pool leaves 8 CUs free; shard batches "
+                         "in the persistent pool instead of a pool grid per batch)")
     ap.add_argument("--multi-device", default=None, metavar="DEVS",
                     help="the one-process multi-GPU path a Rust node uses: ovh_create_multi over DEVS "
                          "('all' = every visible GPU, or e.g. '0,0'), host-buffer batches of --batch votes "
@@ -515,7 +519,9 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
-    ctx = Context(local, flags=OVH_FLAG_PROFILE)
+    sharded = world > 1 or args.shard_path
+    reserve = OVH_FLAG_POOL_RESERVE if args.pool_reserve else 0
+    ctx = Context(local, flags=OVH_FLAG_PROFILE | reserve)
     lib = ctx.lib
     B = args.batch
 
@@ -527,7 +533,7 @@ def main():
     sigs = dev.sign_batch(ctx, sks, hs)
     nbatch = args.warmup + args.steps + args.profile_steps
     codes = torch.full((nbatch, B), -1, dtype=torch.int32, device="cuda")   # one verdict row per batch
-    shards = ShardVerifier(DeviceBackend(ctx)) if (world > 1 or args.shard_path) else None
+    shards = ShardVerifier(DeviceBackend(ctx)) if sharded else None
     # the timed batches' context: the profiling one (HIP events around each batch's pool grids
     # and stages: vote_spans) unless --plain-timed-ctx
     tctx = ctx if (shards is not None or not args.plain_timed_ctx) else Context(local, flags=0)
@@ -694,7 +700,9 @@ def main():
             "data": "synthetic (seed 0xC17A keypairs + RLP precommit votes, SURVEY.md 8(d))",
             "config": {"workload": "config3: %d distinct-message precommit votes per GPU, RLC batch verify" % B,
                        "batch_per_gpu": B, "global_batch": world * B,
-                       "parallelism": "vote shards x%d, partials all-gathered over RCCL" % world if shards is not None
+                       "parallelism": ("vote shards x%d, partials all-gathered over RCCL" % world
+                                       + (", persistent pool leaving 8 CUs to the collective" if reserve
+                                          else ", a pool grid per batch")) if shards is not None
                        else "single GPU"},
             "roofline": {
                 "bound": "valu",

@@ -29,6 +29,8 @@ FLAG_PROFILE = 0x2
 FLAG_VM_TRACE = 0x4
 FLAG_TEST_RLC = 0x8     # tests only: predictable batch coefficients (Context.set_test_rlc)
 FLAG_SK_RAW = 0x10      # private key = raw scalar 0 < sk < r instead of IETF KeyGen
+FLAG_VM_CLOCK = 0x20    # diagnostics: clock stamps around every vote workgroup (pool log)
+FLAG_POOL_RESERVE = 0x40  # the vote pool leaves 8 CUs to the caller's collective (shard contexts)
 
 BLST_ERRORS = {
     1: "BLST_BAD_ENCODING",

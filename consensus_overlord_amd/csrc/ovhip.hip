@@ -446,8 +446,11 @@ struct PoolBatch {  // one published batch (written by k_pool_publish, read by t
 #define PLOG_WG_WORDS 4u
 #define PLOG_GRID_BASE ((size_t)PLOG_RING * PLOG_WORDS)
 #define PLOG_TOTAL (PLOG_GRID_BASE + (size_t)PLOG_GRIDS * (4 + PLOG_WGS * PLOG_WG_WORDS))
+// (the shard path's combine: GATH on the caller's stream when ovh_combine_partials_device_async is
+// called -- after its all-gather --, COMB once the final stream read the partials, FE after the
+// combined check's final exponentiation)
 enum : uint32_t { PLOG_EV_PUB = 0, PLOG_EV_DONE = 1, PLOG_EV_FOLD = 2, PLOG_EV_MSM = 3, PLOG_EV_FINAL = 4,
-                  PLOG_EV_BACK = 5, PLOG_EV_SEQ = 15 };
+                  PLOG_EV_BACK = 5, PLOG_EV_GATH = 6, PLOG_EV_COMB = 7, PLOG_EV_FE = 8, PLOG_EV_SEQ = 15 };
 __global__ void k_grid_hdr(uint64_t* g, uint64_t seq, uint32_t par, uint32_t wgs) {
   for (uint32_t k = threadIdx.x; k < PLOG_WGS * PLOG_WG_WORDS; k += blockDim.x) g[4 + k] = 0;
   __syncthreads();
@@ -481,8 +484,9 @@ struct PoolArgs {
   uint64_t* wlog;  // OVH_FLAG_VM_CLOCK: this grid's workgroup log (PLOG_WG_WORDS per workgroup), else null
   uint64_t only;   // ~0: claim any batch; else this grid's own batch: its workgroups leave once
                    // `cur` has passed it (the shard path's grid per batch, ovh_batch_partial_device)
-  uint32_t nsimd;  // SIMDs of the device (SIMD spreading, pool_claim)
-  uint32_t pad;
+  uint32_t nsimd;  // SIMDs the pool runs on (SIMD spreading, pool_claim)
+  uint32_t skip_cu;  // OVH_FLAG_POOL_RESERVE: workgroups on CUs 0 .. skip_cu - 1 of SE 0 / SA 0 of
+                     // every XCC leave at once (those CUs stay free for other kernels); 0: none
 };
 
 __device__ __forceinline__ uint64_t* pq_done(uint64_t* q, uint32_t slot) { return q + PQ_DONE + slot * POOL_QW; }
@@ -570,7 +574,11 @@ __device__ uint32_t pool_claim(uint64_t* q, const PoolBatch* descs, uint32_t* sl
         *why = idle > POOL_WAIT_TICKS ? 2 : 1;
         return 0;
       }
-      __builtin_amdgcn_s_sleep(8);
+      // past the idle window, poll ~16x less often: 1,700 waiting workgroups polling two queue
+      // words every ~0.2 us kept a shard batch's all-gather and combine from running while the
+      // pool waited for that batch's slot (r06i / r06j pool logs: 20 ms stalls)
+      if (idle > POOL_IDLE_TICKS) __builtin_amdgcn_s_sleep(127);
+      else __builtin_amdgcn_s_sleep(8);
       continue;
     }
     const uint32_t slot = __builtin_amdgcn_readfirstlane(
@@ -833,6 +841,8 @@ __device__ __forceinline__ void vote_quad(const PoolArgs& a, uint32_t slot_in, u
 __global__ __launch_bounds__(64, 2) void k_vm_pool(PoolArgs a) {
   __builtin_amdgcn_s_setprio(2);  // above the final streams' fold checks, below k_vm_final (3)
   extern __shared__ uint4 lds4[];
+  // reserved CUs (OVH_FLAG_POOL_RESERVE): simd_key bits 2..8 = SE | SA | CU (wave-uniform)
+  if (a.skip_cu && ((simd_key() >> 2) & 0x7Fu) < a.skip_cu) return;
   uint32_t* lds = reinterpret_cast<uint32_t*>(lds4);
   load_consts(lds, a.cst, VM_NCONST);
   const uint64_t t_in = __builtin_amdgcn_s_memrealtime();
@@ -2413,8 +2423,12 @@ struct ovh_ctx {
   void* pool_desc = nullptr;
   uint32_t* pool_scr = nullptr;
   uint32_t pool_wgs = 0;
-  uint32_t pool_grid0 = 0;
-  uint32_t ncu = 256;  // workgroups of pool stream 0's grid (4 per CU); stream 1's: 2 pool_wgs - it
+  uint32_t pool_grid0 = 0;  // workgroups of pool stream 0's grid (4 per CU); stream 1's: 2 pool_wgs - it
+  uint32_t ncu = 256;
+  // OVH_FLAG_POOL_RESERVE: CUs left free of the pool, pool_rsv / 8 per XCC (0: none), and the
+  // CUs the pool runs on (ncu - pool_rsv: SIMD spreading)
+  uint32_t pool_rsv = 0;
+  uint32_t pool_ncu = 256;
   uint64_t pool_seq = 0;
   uint32_t* pool_err = nullptr;
   uint64_t* plog = nullptr;  // OVH_FLAG_VM_CLOCK: the pool log (PLOG_RING records)
@@ -2491,6 +2505,10 @@ struct ovh_ctx {
   // 0: off; 1 (default): batches above small_max votes (below it the small-batch path has the
   // lower latency); 2: every batch with at most n / 2 distinct hashes
   int samemsg = 1;
+  // the shard path's grid per batch also claims the next shard_span batches' quads (OVH_SHARD_SPAN,
+  // A/B): it leaves once batch seq + shard_span is claimed, so the grid two batches on finds the
+  // stream free while the caller's collective still gets places between grids
+  uint32_t shard_span = 0;
   // a pool batch's signatures | keys | table indices, staged per slot (k_pool_stage; views)
   uint8_t* pstage[OVH_BATCH_SLOTS] = {};
   uint64_t sm_batches = 0, sm_votes = 0, sm_hashes = 0;
@@ -3080,8 +3098,11 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   const uint32_t wgs = c->pool_wgs;
   PoolArgs pa;
   pa.only = ~0ull;
-  pa.nsimd = 4 * c->ncu;
-  pa.pad = 0;
+  pa.nsimd = 4 * c->pool_ncu;
+  pa.skip_cu = c->pool_rsv / 8;
+  // a grid per shard batch unless the pool leaves CUs to the collective (OVH_FLAG_POOL_RESERVE):
+  // then shard batches share the persistent pool like the others
+  shard = shard && !c->pool_rsv;
   pa.q = c->pool_q;
   pa.descs = (const PoolBatch*)c->pool_desc;
   pa.pv_code = c->vm_vote.code;
@@ -3091,11 +3112,12 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   pa.fold_code = c->vm_fold.code;
   pa.cst = c->vm_consts;
   for (uint32_t par = 0; launch && par < 2; ++par) {
-    // the shard path: one grid of this batch alone per batch, on the pool streams in turn (its
-    // workgroups leave when the batch is claimed, so the caller's collective finds places between
-    // batches -- with persistent grids it waited for the pool to drain, r05an / r05aq pool logs)
+    // the shard path without reserved CUs: one grid of this batch alone per batch, on the pool
+    // streams in turn (its workgroups leave when the batch is claimed, so the caller's collective
+    // finds places between batches -- with persistent grids and the pool on every CU it waited for
+    // the pool to drain, r05an / r05aq pool logs)
     if (shard && par != (uint32_t)(seq & 1)) continue;
-    if (shard) pa.only = seq;
+    if (shard) pa.only = seq + c->shard_span;
     hipStream_t pst = c->pool_st[par];
     HIPCHK(hipStreamWaitEvent(pst, c->ev_front[slot], 0));
     if (par == 0 || shard) {  // the vote stage's and the vote spans' start (stream 0), end (stream 1)
@@ -4208,6 +4230,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   // same-message routing
   if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
   if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e);
+  if (const char* e = getenv("OVH_SHARD_SPAN")) c->shard_span = (uint32_t)atoi(e);
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
   // the pool: eight vote workgroups fit a CU (LDS); POOL_HOLES_PER_8CU of every eight CUs' 64
@@ -4215,7 +4238,19 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   // and hash_to_field of the next batches, which would otherwise wait for the pool to drain. The
   // pool's places are split between the grids of the two pool streams (batch_front), which run
   // side by side: each grid holds half of them
-  c->pool_wgs = ((uint32_t)ncu * 8 - (uint32_t)ncu * POOL_HOLES_PER_8CU / 8) / 2;
+  // OVH_FLAG_POOL_RESERVE: pool_rsv / 8 CUs of every XCC left free of the pool -- its workgroups
+  // that land there leave at once (k_vm_pool; a CU mask on the pool streams made them blocking
+  // streams on separate queues that ran one batch at a time, r06e-g); the grids keep their sizes,
+  // so the dispatcher still deals them evenly. OVH_POOL_PER_CU (A/B): 8 = no holes on the others
+  if (flags & OVH_FLAG_POOL_RESERVE) {
+    c->pool_rsv = 8;
+    if (const char* e = getenv("OVH_POOL_RESERVE")) c->pool_rsv = (uint32_t)atoi(e);
+    if (c->pool_rsv % 8 || c->pool_rsv > 64 || (uint32_t)ncu <= 2 * c->pool_rsv) c->pool_rsv = 0;
+  }
+  const uint32_t pncu = (uint32_t)ncu - c->pool_rsv;
+  uint32_t holes = POOL_HOLES_PER_8CU;
+  if (const char* e = c->pool_rsv ? getenv("OVH_POOL_PER_CU") : nullptr) holes = atoi(e) == 8 ? 0u : holes;
+  c->pool_wgs = ((uint32_t)ncu * 8 - (uint32_t)ncu * holes / 8) / 2;
   if (c->pool_wgs > POOL_MAX_WGS) c->pool_wgs = POOL_MAX_WGS;
   // the two grids as 4 + 3 workgroups per CU rather than 3.5 + 3.5: a grid of a whole number of
   // workgroups per CU is dealt evenly (one per SIMD), so every SIMD holds a pool wave -- with two
@@ -4223,6 +4258,7 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   // on ~90 SIMDs (5.6 ms against 3.8 for a quad alone, r05az)
   c->pool_grid0 = std::min(4u * (uint32_t)ncu, 2 * c->pool_wgs - 1);
   c->ncu = (uint32_t)ncu;
+  c->pool_ncu = pncu;
   if (!dst) {
     dst = DEFAULT_DST;
     dst_len = 43;
@@ -5564,6 +5600,7 @@ int ovh_combine_partials_device_async(ovh_ctx* c, size_t k, const uint8_t* d_par
   const int slot = c->last_slot;
   hipStream_t st = (hipStream_t)stream, fst = c->fs[slot];
   if (st) {  // the partials are complete in `st` order (after the caller's all-gather)
+    plog_stamp(c, slot, PLOG_EV_GATH, st);
     HIPCHK(hipEventRecord(c->ev_x[2], st));
     HIPCHK(hipStreamWaitEvent(fst, c->ev_x[2], 0));
   }
@@ -5571,12 +5608,14 @@ int ovh_combine_partials_device_async(ovh_ctx* c, size_t k, const uint8_t* d_par
   Slab F, S;
   uint32_t m;
   CHK(stage_partials(c, fst, k, d_partials, scratch, &F, &S, &m));
+  plog_stamp(c, slot, PLOG_EV_COMB, fst);
   if (st) {  // the caller may reuse d_partials once they were read
     HIPCHK(hipEventRecord(c->ev_x[3], fst));
     HIPCHK(hipStreamWaitEvent(st, c->ev_x[3], 0));
   }
   int32_t* verdict = c->result + RES_COMBINE + slot;
   enqueue_final(c, fst, F, S, m, verdict);
+  plog_stamp(c, slot, PLOG_EV_FE, fst);
   if (n) enqueue_bisect(c, fst, slot, (uint32_t)n, d_codes, verdict);
   plog_stamp(c, slot, PLOG_EV_BACK, fst);
   HIPCHK(hipEventRecord(c->ev_back[slot], fst));

@@ -55,6 +55,12 @@ typedef struct ovh_ctx ovh_ctx;
                                            SecretKey::from_bytes) instead of KeyGen (see ovh_sk_parse) */
 #define OVH_FLAG_VM_CLOCK 0x20u         /* diagnostics: shader / wall clock stamps around every vote
                                            workgroup's program (ovh_vm_clock) */
+#define OVH_FLAG_POOL_RESERVE 0x40u     /* the vote pool leaves 8 compute units (one per XCD; env
+                                           OVH_POOL_RESERVE: another multiple of 8, <= 64) free for
+                                           other kernels -- the caller's collective between shard
+                                           batches -- and shard batches (ovh_batch_partial_device*,
+                                           ovh_create_multi) share the persistent pool instead of a grid
+                                           per batch. Use for a context whose partials cross RCCL. */
 
 /* Batch stages (ovh_stage_name gives the label). Each stage is one or more kernels. */
 #define OVH_NSTAGES 6

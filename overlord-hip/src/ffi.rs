@@ -26,6 +26,8 @@ pub const OVH_FLAG_VM_TRACE: u32 = 0x4;
 pub const OVH_FLAG_TEST_RLC: u32 = 0x8;
 pub const OVH_FLAG_SK_RAW: u32 = 0x10;
 pub const OVH_FLAG_VM_CLOCK: u32 = 0x20;
+/// The vote pool on CU-masked streams leaving 8 CUs to other kernels (RCCL between shard batches).
+pub const OVH_FLAG_POOL_RESERVE: u32 = 0x40;
 
 pub const OVH_NSTAGES: usize = 6;
 pub const OVH_VOTE_HASH_MAX: usize = 64;

@@ -291,13 +291,14 @@ def test_partials_interoperate_with_oracle(cc):
 def test_shard_verifier_rccl_single_rank(cc):
     """The multi-GPU driver (consensus_overlord_amd/shard.py) on the GPU with libovhip as the
     backend, over a one-rank RCCL group: pipelined shard batches (one with invalid votes) give
-    the per-vote codes."""
+    the per-vote codes, with the test's context and with an OVH_FLAG_POOL_RESERVE one."""
     import os
     import socket
     import torch
     import torch.distributed as dist
     import bls12_381 as bls
     from consensus_overlord_amd import device as dev
+    from consensus_overlord_amd.crypto import Context, FLAG_POOL_RESERVE
     from consensus_overlord_amd.shard import DeviceBackend, ShardVerifier
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -313,15 +314,20 @@ def test_shard_verifier_rccl_single_rank(cc):
         pt = bls.g2_from_bytes(bytes(s_host[9]))
         s_host[9] = np.frombuffer(bls.g2_compress(bls.pt_add(bls.Fp2Ops, pt, bls.G2_GEN)), dtype=np.uint8)
         bad = torch.from_numpy(s_host).cuda()
-        sv = ShardVerifier(DeviceBackend(cc.ctx))
-        codes = torch.full((3, n), -1, dtype=torch.int32, device="cuda")
-        torch.cuda.synchronize()
-        for b, sg in enumerate((sigs, bad, sigs)):
-            sv.submit(b, sg, hs, pks, codes[b])
-        sv.wait()
-        c = codes.cpu().numpy()
-        assert (c[0] == 0).all() and (c[2] == 0).all()
-        assert [i for i in range(n) if c[1, i] != 0] == [9] and c[1, 9] == 5
+        # the test's context, then one whose pool leaves CUs to the collective (OVH_FLAG_POOL_RESERVE:
+        # shard batches in the persistent pool, bench.py's shard path)
+        rsv = Context(0, flags=FLAG_POOL_RESERVE)
+        for ctx in (cc.ctx, rsv):
+            sv = ShardVerifier(DeviceBackend(ctx))
+            codes = torch.full((3, n), -1, dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()
+            for b, sg in enumerate((sigs, bad, sigs)):
+                sv.submit(b, sg, hs, pks, codes[b])
+            sv.wait()
+            c = codes.cpu().numpy()
+            assert (c[0] == 0).all() and (c[2] == 0).all()
+            assert [i for i in range(n) if c[1, i] != 0] == [9] and c[1, 9] == 5
+        rsv.close()
     finally:
         dist.destroy_process_group()
 

@@ -142,18 +142,21 @@ def test_pinned_host_inputs_on_ovh_stream_then_close(votes):
             assert got[k].tolist() == want_bad.tolist(), k
 
 
-def test_async_batch_then_shard_partial_without_wait(votes):
+@pytest.mark.parametrize("reserve", [False, True])
+def test_async_batch_then_shard_partial_without_wait(votes, reserve):
     """a pipelined batch (persistent pool grids) and, with no ovh_batch_wait
     between them, a shard batch (ovh_batch_partial_device on a stream: a grid of its own on the
     other pool stream) are in the pool together. Each pool stream has its own fixed spill-scratch
-    region, so no two co-resident workgroups share one; both batches' codes equal the oracle's."""
+    region, so no two co-resident workgroups share one; both batches' codes equal the oracle's.
+    reserve: the same on an OVH_FLAG_POOL_RESERVE context (CU-masked pool streams; the shard batch
+    joins the persistent pool)."""
     import torch
     from consensus_overlord_amd import device as dev
-    from consensus_overlord_amd.crypto import Context
+    from consensus_overlord_amd.crypto import Context, FLAG_POOL_RESERVE
     s, h, p = votes
     n = len(s)
     bad_s, bad_p, want_bad = _bad_jobs(votes)
-    ctx = Context(0)
+    ctx = Context(0, flags=FLAG_POOL_RESERVE if reserve else 0)
     d_h = torch.from_numpy(h).cuda()
     a_s, a_p = torch.from_numpy(bad_s).cuda(), torch.from_numpy(bad_p).cuda()
     b_s, b_p = torch.from_numpy(s).cuda(), torch.from_numpy(p).cuda()
@@ -174,3 +177,50 @@ def test_async_batch_then_shard_partial_without_wait(votes):
     assert codes_b.cpu().numpy().tolist() == want_bad.tolist()
     assert (codes_c.cpu().numpy() == 0).all()
     ctx.close()
+
+
+def test_reserved_pool_shard_pipeline_with_gather_copies(votes):
+    """OVH_FLAG_POOL_RESERVE (include/ovhip.h): eight shard batches -- more than the context's
+    batch slots -- pipelined on one stream as bench.py's shard path runs them: partial, a
+    device copy of the partial standing in for the RCCL all-gather (a kernel that needs CU places
+    beside the persistent pool), combine. Batches 2 and 5 carry invalid votes; every batch's codes
+    equal the oracle's. Then the masked streams are parked and taken back: an unreserved context
+    in between runs a batch of its own on unmasked streams."""
+    import torch
+    from consensus_overlord_amd import device as dev
+    from consensus_overlord_amd.crypto import Context, FLAG_POOL_RESERVE
+    s, h, p = votes
+    n = len(s)
+    bad_s, bad_p, want_bad = _bad_jobs(votes)
+    d_h = torch.from_numpy(h).cuda()
+    good = (torch.from_numpy(s).cuda(), torch.from_numpy(p).cuda())
+    bad = (torch.from_numpy(bad_s).cuda(), torch.from_numpy(bad_p).cuda())
+    for rep in range(2):
+        ctx = Context(0, flags=FLAG_POOL_RESERVE)
+        nb = 8
+        codes = torch.full((nb, n), -1, dtype=torch.int32, device="cuda")
+        mine = torch.zeros((nb, 864), dtype=torch.uint8, device="cuda")
+        gathered = torch.zeros((nb, 1, 864), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        st = torch.cuda.Stream()
+        with torch.cuda.stream(st):
+            for b in range(nb):
+                sg, pk = bad if b in (2, 5) else good
+                dev.batch_partial(ctx, sg, d_h, pk, codes[b], mine[b], stream=True)
+                gathered[b, 0].copy_(mine[b])
+                dev.combine_partials_async(ctx, gathered[b], n, codes[b], stream=True)
+        dev.batch_wait(ctx)
+        torch.cuda.synchronize()
+        got = codes.cpu().numpy()
+        for b in range(nb):
+            want = want_bad.tolist() if b in (2, 5) else [0] * n
+            assert got[b].tolist() == want, (rep, b)
+        ctx.close()
+        if rep == 0:
+            other = Context(0)
+            c2 = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+            dev.verify_batch_async(other, bad[0], d_h, bad[1], c2)
+            dev.batch_wait(other)
+            torch.cuda.synchronize()
+            assert c2.cpu().numpy().tolist() == want_bad.tolist()
+            other.close()

@@ -4,7 +4,9 @@ batches through ovh_verify_batch_device_async -- on an OVH_FLAG_VM_CLOCK context
 pool log (ovh_pool_log): per batch its publication, first quad start, last quad end and the final
 stream's events, plus the quads in flight over time. One JSON object per run on stdout.
 
-    python tools/pool_timeline.py [K] [runs] > gpurun_out/timeline.json
+    python tools/pool_timeline.py [K] [runs] [shard [rsv]] > gpurun_out/timeline.json
+
+shard: through the shard driver at one RCCL rank; rsv: on an OVH_FLAG_POOL_RESERVE context.
 """
 import ctypes
 import json
@@ -18,7 +20,7 @@ sys.path.insert(0, ROOT)
 RING, QUADS, WORDS = 64, 1024, 16 + 2 * 1024
 GRIDS, WGS, WGW = 64, 1024, 4
 TOTAL = RING * WORDS + GRIDS * (4 + WGS * WGW)
-EV = ["pub", "done", "fold", "msm", "final", "back"]
+EV = ["pub", "done", "fold", "msm", "final", "back", "gath", "comb", "fe"]
 
 
 def one_run(c, dev, sigs, hs, pks, K, codes):
@@ -108,7 +110,8 @@ def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     runs = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     shard = len(sys.argv) > 3 and sys.argv[3] == "shard"
-    c = Context(0, flags=bench.OVH_FLAG_PROFILE | bench.OVH_FLAG_VM_CLOCK)
+    rsv = bench.OVH_FLAG_POOL_RESERVE if len(sys.argv) > 4 and sys.argv[4] == "rsv" else 0
+    c = Context(0, flags=bench.OVH_FLAG_PROFILE | bench.OVH_FLAG_VM_CLOCK | rsv)
     sks_h, hs_h = bench.synth_inputs(c.lib, 0, 4096)
     sks = torch.from_numpy(sks_h).cuda()
     hs = torch.from_numpy(hs_h).cuda()
