@@ -2399,6 +2399,7 @@ struct HostBatch {
   std::vector<Dev> dev;
 };
 
+#define NFIN_STREAMS 4u
 struct ovh_ctx {
   int device = 0;
   uint32_t flags = 0;
@@ -2409,6 +2410,8 @@ struct ovh_ctx {
   // batch state rotate (a slot is reused only after its final-stream work finished). Batches
   // take the NFIN_STREAMS final streams in turn, so that many chains run at once.
   hipStream_t fstream = nullptr, fstream2 = nullptr, fstream3 = nullptr;
+  hipStream_t fstream4 = nullptr;
+  uint32_t nfin = NFIN_STREAMS;  // final streams in turn (OVH_NFIN: 2, 3 or 4, A/B)
   hipStream_t xstream = nullptr;  // per-call side work beside `stream` (aggregate_signatures' key parse; lazy)
   // ovh_verify_samemsg_device_async: [0], [1] the per-vote streams, in turn; [2] hash_to_G2 (lazy)
   hipStream_t vstream[3] = {};
@@ -2418,7 +2421,7 @@ struct ovh_ctx {
   // workgroups' spill scratch (2 x pool_wgs x 4 x VOTE_NSCR entries: one area per pool stream),
   // the grid size, the next batch's sequence number, and the timeout flag of k_pool_wait
   // (coherent host memory)
-  hipStream_t pool_st[2] = {};  // every batch has a pool grid on each (see batch_front)
+  hipStream_t pool_st[3] = {};  // every batch has a pool grid on [0] and [1] (see batch_front); [2]: OVH_SHARD_STREAMS
   uint64_t* pool_q = nullptr;
   void* pool_desc = nullptr;
   uint32_t* pool_scr = nullptr;
@@ -2509,6 +2512,8 @@ struct ovh_ctx {
   // A/B): it leaves once batch seq + shard_span is claimed, so the grid two batches on finds the
   // stream free while the caller's collective still gets places between grids
   uint32_t shard_span = 0;
+  // pool streams the shard path's grids rotate over (OVH_SHARD_STREAMS, A/B: 2 or 3)
+  uint32_t shard_streams = 2;
   // a pool batch's signatures | keys | table indices, staged per slot (k_pool_stage; views)
   uint8_t* pstage[OVH_BATCH_SLOTS] = {};
   uint64_t sm_batches = 0, sm_votes = 0, sm_hashes = 0;
@@ -2864,8 +2869,9 @@ static int sync_all(ovh_ctx* c) {
   HIPCHK(hipStreamSynchronize(c->fstream));
   HIPCHK(hipStreamSynchronize(c->fstream2));
   HIPCHK(hipStreamSynchronize(c->fstream3));
-  for (hipStream_t s : {c->pool_st[0], c->pool_st[1], c->vstream[0], c->vstream[1], c->vstream[2], c->hstream[1],
-                        c->hstream[2], c->hstream[3]})
+  if (c->fstream4) HIPCHK(hipStreamSynchronize(c->fstream4));
+  for (hipStream_t s : {c->pool_st[0], c->pool_st[1], c->pool_st[2], c->vstream[0], c->vstream[1], c->vstream[2],
+                        c->hstream[1], c->hstream[2], c->hstream[3]})
     if (s) HIPCHK(hipStreamSynchronize(s));
   return pool_failed(c);
 }
@@ -2979,13 +2985,14 @@ static int ensure_in(ovh_ctx* c, size_t bytes) {
 // final stream has finished with the slot's previous batch (its bisection reads that state).
 // final streams: a batch's fold levels, MSM, final and bisection take 4-6 ms beside the pool
 // (r05y pool log), so two in turn held the pipeline to one batch per ~3 ms; three: 1,378k-1,386k
-// verifs/s vs 1,254k-1,260k (r05z)
-#define NFIN_STREAMS 3u
+// verifs/s vs 1,254k-1,260k (r05z). Four (the low-priority hardware queues' count): the pool path
+// unchanged (1,600-1,608k vs 1,607-1,608k), pipelined same-message batches 1.58-1.62 ms per
+// batch against 1.82-1.84 (r06o)
 static int take_slot(ovh_ctx* c, int* slot) {
   const int k = (int)(c->pipe_k % OVH_BATCH_SLOTS);
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_back[k], 0));
-  const uint64_t f = c->pipe_k % NFIN_STREAMS;
-  c->fs[k] = f == 0 ? c->fstream : f == 1 ? c->fstream2 : c->fstream3;
+  const uint64_t f = c->pipe_k % c->nfin;
+  c->fs[k] = f == 0 ? c->fstream : f == 1 ? c->fstream2 : f == 2 ? c->fstream3 : c->fstream4;
   ++c->pipe_k;
   c->last_slot = k;
   *slot = k;
@@ -3111,12 +3118,12 @@ static int batch_front(ovh_ctx* c, int slot, uint32_t n, const uint8_t* d_sigs, 
   pa.pt_side = c->vm_vote_t.side;
   pa.fold_code = c->vm_fold.code;
   pa.cst = c->vm_consts;
-  for (uint32_t par = 0; launch && par < 2; ++par) {
+  for (uint32_t par = 0; launch && par < (shard ? c->shard_streams : 2u); ++par) {
     // the shard path without reserved CUs: one grid of this batch alone per batch, on the pool
     // streams in turn (its workgroups leave when the batch is claimed, so the caller's collective
     // finds places between batches -- with persistent grids and the pool on every CU it waited for
     // the pool to drain, r05an / r05aq pool logs)
-    if (shard && par != (uint32_t)(seq & 1)) continue;
+    if (shard && par != (uint32_t)(seq % c->shard_streams)) continue;
     if (shard) pa.only = seq + c->shard_span;
     hipStream_t pst = c->pool_st[par];
     HIPCHK(hipStreamWaitEvent(pst, c->ev_front[slot], 0));
@@ -3666,6 +3673,8 @@ static int verify_samemsg_locked(ovh_ctx* c, int slot, size_t n, const uint8_t* 
   // stream consecutive batches' hash_to_G2 ran back to back)
   const uint32_t hk = one ? (uint32_t)(c->pipe_k % SM_H2G_STREAMS) : 0u;
   if (hk && !c->hstream[hk]) HIPCHK(stream_new(&c->hstream[hk], 0));
+  // (the one-hash path's key sums on the final stream: on the side stream, beside the MSM, a
+  // pipelined batch took 1.78-1.81 ms against 1.57-1.63, r06p)
   const hipStream_t xs = one ? fst : c->xstream, hs = hk ? c->hstream[hk] : c->xstream;
   HIPCHK(hipEventRecord(c->ev_front[slot], c->stream));  // the inputs (and the slot free: take_slot)
   HIPCHK(hipStreamWaitEvent(hs, c->ev_front[slot], 0));
@@ -4231,6 +4240,8 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
   if (const char* e = getenv("OVH_SMALL_MAX")) c->small_max = (uint32_t)atoi(e);
   if (const char* e = getenv("OVH_SAMEMSG")) c->samemsg = atoi(e);
   if (const char* e = getenv("OVH_SHARD_SPAN")) c->shard_span = (uint32_t)atoi(e);
+  if (const char* e = getenv("OVH_SHARD_STREAMS")) c->shard_streams = atoi(e) == 3 ? 3u : 2u;
+  if (const char* e = getenv("OVH_NFIN")) c->nfin = atoi(e) == 3 ? 3u : atoi(e) == 2 ? 2u : NFIN_STREAMS;
   int ncu = 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
   // the pool: eight vote workgroups fit a CU (LDS); POOL_HOLES_PER_8CU of every eight CUs' 64
@@ -4272,14 +4283,16 @@ ovh_ctx* ovh_create(int device, const uint8_t* dst, size_t dst_len, uint32_t fla
             stream_new(&c->fstream, lo) == hipSuccess &&
             stream_new(&c->fstream2, lo) == hipSuccess &&
             stream_new(&c->fstream3, lo) == hipSuccess &&
+            (c->nfin < 4 || stream_new(&c->fstream4, lo) == hipSuccess) &&
             stream_new(&c->pool_st[0], hi) == hipSuccess &&
             stream_new(&c->pool_st[1], hi) == hipSuccess &&
+            (c->shard_streams < 3 || stream_new(&c->pool_st[2], hi) == hipSuccess) &&
             hipMalloc(&c->part_out, (size_t)OVH_BATCH_SLOTS * 2 * 216 * 4) == hipSuccess && hipMalloc(&c->result, RES_WORDS * 4) == hipSuccess &&
             hipMemset(c->result, 0, RES_WORDS * 4) == hipSuccess &&
             hipMalloc(&c->pool_q, (size_t)PQ_WORDS * 8) == hipSuccess && hipMemset(c->pool_q, 0, (size_t)PQ_WORDS * 8) == hipSuccess &&
             hipMalloc(&c->pool_desc, sizeof(PoolBatch) * OVH_BATCH_SLOTS) == hipSuccess &&
             hipMemset(c->pool_desc, 0, sizeof(PoolBatch) * OVH_BATCH_SLOTS) == hipSuccess &&
-            hipMalloc(&c->pool_scr, (size_t)4 * c->pool_wgs * VM_SLICES * VOTE_NSCR * 48) == hipSuccess &&
+            hipMalloc(&c->pool_scr, (size_t)2 * c->shard_streams * c->pool_wgs * VM_SLICES * VOTE_NSCR * 48) == hipSuccess &&
             hipHostMalloc((void**)&c->pool_err, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
             hipMalloc(&c->fin, (size_t)OVH_BATCH_SLOTS * FIN_STRIDE * 4) == hipSuccess && vm_init(c) == 0;
   if (ok) *c->pool_err = 0;
@@ -4375,8 +4388,8 @@ int ovh_multi_peer_matrix(ovh_ctx* c, uint8_t* out, size_t cap) {
 static void destroy_one(ovh_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
-                        c->pool_st[1], c->hstream[1], c->hstream[2], c->hstream[3]})
+  for (hipStream_t s : {c->fstream, c->fstream2, c->fstream3, c->fstream4, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2], c->pool_st[0],
+                        c->pool_st[1], c->pool_st[2], c->hstream[1], c->hstream[2], c->hstream[3]})
     if (s) (void)hipStreamSynchronize(s);
   for (int k = 0; k < OVH_BATCH_SLOTS; ++k)
     for (void* p : {(void*)c->grp_ok[k], (void*)c->msm_buf[k], (void*)c->gslab[k]})
@@ -4411,8 +4424,8 @@ static void destroy_one(ovh_ctx* c) {
     if (c->vev1[k]) (void)hipEventDestroy(c->vev1[k]);
   }
   // the streams are parked, not destroyed (stream_new)
-  for (hipStream_t s : {c->stream, c->fstream, c->fstream2, c->fstream3, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
-                        c->pool_st[0], c->pool_st[1], c->hstream[1], c->hstream[2], c->hstream[3]})
+  for (hipStream_t s : {c->stream, c->fstream, c->fstream2, c->fstream3, c->fstream4, c->xstream, c->vstream[0], c->vstream[1], c->vstream[2],
+                        c->pool_st[0], c->pool_st[1], c->pool_st[2], c->hstream[1], c->hstream[2], c->hstream[3]})
     stream_park(c->device, s);
   if (c->pool_err) (void)hipHostFree(c->pool_err);
   delete c;
