@@ -751,7 +751,7 @@ def main():
             "batch_latency_ms": round(float(np.median(lat)) * 1e3, 3) if lat else None,
             "enqueue_ms_per_step": round(enqueue_s / args.steps * 1e3, 4),
             "pipelined": "the vote pool runs every batch's per-vote work (persistent grids, quads claimed across "
-                         "batches); batch k's fold, MSM, combined check and bisection run on one of three final "
+                         "batches); batch k's fold, MSM, combined check and bisection run on one of four final "
                          "streams beside later batches' votes; all %d timed batches complete inside the timed "
                          "region" % args.steps,
         }
