@@ -308,7 +308,7 @@ def test_spill_pass_bounds_slots_and_keeps_values(hx, built, golden_votes):  # n
     prog.fuse()
     sc = sched.schedule(prog, gen.WIDTH["vote"], consts, max_slots=400, heavy_w=gen.HEAVY_W["vote"],
                         hoist=gen.HOIST["vote"], stretch=gen.STRETCH["vote"], mixed=False, spill_k=K,
-                        defer=gen.DEFER.get("vote"))
+                        defer=gen.DEFER.get("vote"), families="vote" in gen.FAMILIES)
     words = sched.encode(sc)
     assert sc.nslots <= K and sc.nscr > 0 and sc.nfill >= sc.nspill > 0 and sc.nrounds == vsc.nrounds
     spill_at, fill_at = {}, []

@@ -47,13 +47,16 @@ STRETCH = {"gfin": 1.0, "vsame": 1.0, "vsame_t": 1.0, "vsame8": 1.0, "vsame8_t":
 # priority weight of a heavy op against a light one (path length in weighted ops). r03 scan on
 # the cost model (product phase 1.60 us, linear 0.69 us): vote 4 -> 64 estimates 3.29 -> 3.10 ms
 # (a product on the path outweighs any run of light ops); vote_t keeps 2
-HEAVY_W = {"vote": 128, "vote_t": 64, "vsame": 64, "vsame_t": 64, "vsame8": 128, "vsame8_t": 128, "h2g": 64}
+HEAVY_W = {"vote": 48, "vote_t": 64, "vsame": 64, "vsame_t": 64, "vsame8": 128, "vsame8_t": 128, "h2g": 64}
 # heavy-phase deferral (sched.schedule `defer`: h_thr, h_margin, l_thr) for the batch vote
 # programs, whose cost is VALU per quad rather than phases: fuller product phases, more light ones
 # (r06 offline sweep over h_thr, h_margin, l_thr, heavy_w, hoist; vote static VALU per quad
 # 1.136 M -> 1.106 M, vote_t 1.104 M -> 1.097 M; the same-message per-vote programs vsame8
 # 697 k -> 641 k per wave, vsame8_t 524 k -> 485 k)
-DEFER = {"vote": (16, 1e4, 6), "vote_t": (16, 1e4, 8), "vsame8": (8, 1e4, 1), "vsame8_t": (8, 1e4, 1)}
+DEFER = {"vote": (16, 1e4, 8), "vote_t": (16, 1e4, 8), "vsame8": (8, 1e4, 1), "vsame8_t": (8, 1e4, 1)}
+# block families (sched.schedule `families`): fill a phase from the ops no costlier than its top
+# op's first (vote 1.106 M -> 1.098 M, vote_t 1.097 M -> 1.093 M static; vsame8 gains nothing)
+FAMILIES = {"vote", "vote_t"}
 # list-scheduling priority offsets per program section (ir.Prog.section): the signature's
 # decompression + subgroup check has no successor, so by path length alone it loses every
 # contended phase to the Miller loop and ends up as a latency-bound tail; the offset runs it in
@@ -97,7 +100,8 @@ def build_all():
                 if name in SEC_BIAS and op.sec in SEC_BIAS[name]}
         sc = sched.schedule(prog, WIDTH[name], consts, max_slots=MAX_SLOTS.get(name, 256), heavy_w=HEAVY_W.get(name, 2),
                             hoist=HOIST.get(name), stretch=STRETCH.get(name, 1.3), mixed=name not in NOMIX,
-                            bias=bias or None, spill_k=SPILL_K.get(name) or None, defer=DEFER.get(name))
+                            bias=bias or None, spill_k=SPILL_K.get(name) or None, defer=DEFER.get(name),
+                            families=name in FAMILIES)
         words = sched.encode(sc)
         out[name] = (prog, sc, words, ins, outs)
     return consts, out

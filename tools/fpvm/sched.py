@@ -100,7 +100,7 @@ class Scheduled:
 
 def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1, mixed=True, slot_target=None,
              hoist=None, stretch=1.3, split_sop=False, dual=False, bias=None, light_margin=0, spill_k=None,
-             defer=None):
+             defer=None, families=False):
     ops = prog.ops
     live = prog.live_ops()
     liveset = set(live)
@@ -158,6 +158,16 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
     def pick(cands, n, pressure):
         if not cands or n <= 0:
             return []
+        if families and not pressure:
+            cands.sort(key=lambda i: -prio[i])
+            top = fam[cands[0]]
+            take = [i for i in cands if fam[i] <= top][:n]
+            if len(take) < n and families != "strict":
+                ts = set(take)
+                take += [i for i in cands if i not in ts][:n - len(take)]
+            ts = set(take)
+            cands[:] = [i for i in cands if i not in ts]
+            return take
         if pressure:
             cands.sort(key=lambda i: (delta(i), -prio[i]))
             take = cands[:n]
@@ -173,6 +183,22 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
     # (16, 1e4, 6): 1,375 -> 1,289 product phases (lane use 0.833 -> 0.888), 1,307 -> 1,460 light
     # phases, 1,281 -> 299 spills; static VALU per quad 1.136 M -> 1.106 M (tools/valu_attr.py)
     h_thr, h_margin, l_thr = defer if defer is not None else (0, 0, 1)
+    # families (r06): the interpreter's wave-uniform blocks cost by the costliest lane of a phase --
+    # a product with a negated operand (pre_add2's 2p - D chain, 51 VALU against 24), a unit lin
+    # with a negated term (lin_sum 94 against 37), a general-coefficient lin (lin_mad: every lin
+    # of its phase) -- so a phase is filled from the ops no costlier than its top op's first
+    fam = {}
+    if families:
+        for i in work:
+            k = ops[i].kind
+            if k in PRODUCTS:
+                cf = lane_operands(prog, i)[4]
+                fam[i] = 1 if (k == "eq" or cf[1] < 0 or cf[3] < 0) else 0
+            elif k == "lin":
+                form = lin_form(prog._lin_terms(ops[i]), prog.lin_width)
+                fam[i] = 2 if form[0] == "acc" else (1 if any(c < 0 for c, _ in form[-1]) else 0)
+            else:
+                fam[i] = 0
     rounds = []
     kinds = []
     done = 0
