@@ -278,28 +278,56 @@ VM_FN void pre_add2(Fp& x, const Fp& A, const Fp& B, Fp& y, const Fp& C, const F
   }
 }
 
+// phase header bits (w0 bits 22..31, tools/fpvm/sched.py H_*)
+constexpr uint32_t H_MUL = 1u << 22, H_MULNEG = 1u << 23, H_FLAG = 1u << 24, H_LIN = 1u << 25,
+                   H_LINNEG = 1u << 26, H_ACC = 1u << 27, H_RARE = 1u << 28, H_SELB = 1u << 29,
+                   H_LINNEG2 = 1u << 30, H_LINNEG3 = 1u << 31;
+constexpr uint32_t H_ANY = H_MUL | H_LIN | H_ACC | H_RARE;
+
+// The negated-sum chain of lin_sum: XB / XC XOR B / C with their masks (D always): a unit sum's
+// negated terms sit in the last positions (tools/fpvm/sched.py lane_operands), so the phase
+// header (H_LINNEG2: some lane negates C, H_LINNEG3: B) skips the XORs no lane needs.
+template <bool XB, bool XC>
+VM_FN void lin_chain_neg(uint32_t* s, const Fp& A, const Fp& B, const Fp& C, const Fp& D, uint32_t mb, uint32_t mc,
+                         uint32_t md, const Fp& K) {
+  uint32_t u[12], v[12], w[12], c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+#pragma unroll
+  for (int j = 0; j < 14; ++j) {
+    if (j < 12) {
+      u[j] = addc32(A.v[j], XB ? B.v[j] ^ mb : B.v[j], c1, &c1);
+      v[j] = addc32(XC ? C.v[j] ^ mc : C.v[j], D.v[j] ^ md, c2, &c2);
+    }
+    if (j >= 1 && j <= 12) w[j - 1] = addc32(u[j - 1], v[j - 1], c3, &c3);
+    if (j >= 2) s[j - 2] = addc32(w[j - 2], K.v[j - 2], c4, &c4);
+  }
+}
+
 // s = A + sb B + sc C + sd D with unit signs (a zero coefficient points its operand at the zero
 // constant), s < 8p in 12 limbs: a negated term enters as ~X (mb, mc, md: all-ones masks of the
 // negated terms; a unit sum's first term is never negated, ir._expand_unit) and the offset
 // K = n (2p + 1) (n negated terms, constant-table entry KTAB + n) turns each ~X into 2p - X
 // modulo 2^384. Four carry chains (A + B', C' + D', their sum, + K) skewed by one limb each.
 VM_FN void lin_sum(uint32_t* s, const Fp& A, const Fp& B, const Fp& C, const Fp& D, uint32_t mb, uint32_t mc,
-                   uint32_t md, bool any_neg, const uint32_t* __restrict__ cst) {
-  uint32_t u[12], v[12], w[12], c1 = 0, c2 = 0, c3 = 0, c4 = 0;
-  if (any_neg) {
+                   uint32_t md, uint32_t hdr, const uint32_t* __restrict__ cst) {
+  if (hdr & H_LINNEG) {
     const uint32_t n = (mb & 1u) + (mc & 1u) + (md & 1u);
     Fp K;
     ld_slot(K, nullptr, cst, CONST_BASE + KTAB + n);
-#pragma unroll
-    for (int j = 0; j < 14; ++j) {
-      if (j < 12) {
-        u[j] = addc32(A.v[j], B.v[j] ^ mb, c1, &c1);
-        v[j] = addc32(C.v[j] ^ mc, D.v[j] ^ md, c2, &c2);
-      }
-      if (j >= 1 && j <= 12) w[j - 1] = addc32(u[j - 1], v[j - 1], c3, &c3);
-      if (j >= 2) s[j - 2] = addc32(w[j - 2], K.v[j - 2], c4, &c4);
+    if (hdr & H_LINNEG3) {
+      lin_chain_neg<true, true>(s, A, B, C, D, mb, mc, md, K);
+    } else if (hdr & H_LINNEG2) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      __asm__ volatile("");  // (kept branches: three chains, never selects between them)
+#endif
+      lin_chain_neg<false, true>(s, A, B, C, D, mb, mc, md, K);
+    } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+      __asm__ volatile("");
+#endif
+      lin_chain_neg<false, false>(s, A, B, C, D, mb, mc, md, K);
     }
   } else {
+    uint32_t u[12], v[12], c1 = 0, c2 = 0, c3 = 0;
 #pragma unroll
     for (int j = 0; j < 13; ++j) {
       if (j < 12) {
@@ -317,10 +345,6 @@ VM_FN void lin_sum(uint32_t* s, const Fp& A, const Fp& B, const Fp& C, const Fp&
 // constant-table entry). 0 -> 0. `a` must be canonical.
 VM_FN void fp_inv(Fp& r, const Fp& a, const Fp& r3) { fp_inv_divsteps(r, a, r3); }
 
-// phase header bits (w0 bits 22..29, tools/fpvm/sched.py H_*)
-constexpr uint32_t H_MUL = 1u << 22, H_MULNEG = 1u << 23, H_FLAG = 1u << 24, H_LIN = 1u << 25,
-                   H_LINNEG = 1u << 26, H_ACC = 1u << 27, H_RARE = 1u << 28, H_SELB = 1u << 29;
-constexpr uint32_t H_ANY = H_MUL | H_LIN | H_ACC | H_RARE;
 #if defined(__HIPCC__)
 // the header is the same in every lane: read it once into an SGPR
 VM_FN uint32_t uniform(uint32_t w0) { return __builtin_amdgcn_readfirstlane(w0); }
@@ -395,8 +419,7 @@ VM_FN void exec(const uint4 in, bool active, uint32_t* __restrict__ slots, const
   }
   if (hdr & H_LIN) {
     uint32_t s[13];
-    lin_sum(s, A, B, C, D, sign_mask(in.w, 9), sign_mask(in.w, 14), sign_mask(in.w, 19), (hdr & H_LINNEG) != 0,
-            cst);
+    lin_sum(s, A, B, C, D, sign_mask(in.w, 9), sign_mask(in.w, 14), sign_mask(in.w, 19), hdr, cst);
     // "scaled" form k * (unit sum), k < 16 (k <= 1: unchanged; selb: 0)
     const uint32_t k = (in.w >> 20) & 15;
     Fp l;

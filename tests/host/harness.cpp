@@ -109,7 +109,8 @@ void hx_fp_inv_raw(const uint32_t* a, const uint32_t* r_raw, uint32_t* out) {
 int hx_vm_run(const uint32_t* code, uint32_t nphases, uint32_t W, uint32_t NW, const uint32_t* cst, uint32_t* slots,
               uint64_t scalar, uint32_t* planes, uint32_t nplanes, int any_all, const uint32_t* side, uint32_t* scr) {
   using namespace ovh::vm;
-  const uint32_t all = any_all ? (H_MUL | H_MULNEG | H_FLAG | H_LIN | H_LINNEG | H_ACC | H_RARE | H_SELB) : 0u;
+  const uint32_t all =
+      any_all ? (H_MUL | H_MULNEG | H_FLAG | H_LIN | H_LINNEG | H_LINNEG2 | H_LINNEG3 | H_ACC | H_RARE | H_SELB) : 0u;
   const ovh::vm::Out out{planes, 1, 0};
   (void)nplanes;
   for (uint32_t ph = 0; ph < nphases; ++ph) {

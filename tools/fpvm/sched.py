@@ -196,6 +196,7 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
                 fam[i] = 1 if (k == "eq" or cf[1] < 0 or cf[3] < 0) else 0
             elif k == "lin":
                 form = lin_form(prog._lin_terms(ops[i]), prog.lin_width)
+                # unit: the number of negated terms (lin_sum XORs that many positions), general: 4
                 fam[i] = 2 if form[0] == "acc" else (1 if any(c < 0 for c, _ in form[-1]) else 0)
             else:
                 fam[i] = 0
@@ -471,7 +472,11 @@ def lane_operands(prog, i, unit=False):
             srcs = list(op.srcs) + [None] * (LW - len(op.srcs))
             coefs = list(op.coefs) + [0] * (LW - len(op.coefs))
         else:
-            u = form[-1] + [(0, None)] * (LW - len(form[-1]))
+            # r06: negated terms in the last positions (D, then C, then B), so a phase whose lanes
+            # negate at most one or two terms needs no XOR of B / C (phase_bits H_LINNEG2 / 3)
+            pos_ = [t for t in form[-1] if t[0] > 0]
+            neg_ = [t for t in form[-1] if t[0] < 0]
+            u = pos_ + [(0, None)] * (LW - len(pos_) - len(neg_)) + neg_
             srcs = [v for _, v in u]
             coefs = [c for c, _ in u]
             if form[0] == "scaled":
@@ -603,6 +608,9 @@ def encode(sc):
 
 # phase header bits (fpvm.hpp exec): which interpreter blocks any lane of the phase needs
 H_MUL, H_MULNEG, H_FLAG, H_LIN, H_LINNEG, H_ACC, H_RARE, H_SELB = (1 << k for k in range(22, 30))
+# r06: which unit-lin positions some lane negates beyond D (fpvm.hpp lin_sum XORs only those):
+# C (H_LINNEG2) and B (H_LINNEG3); lane_operands puts a unit sum's negated terms last
+H_LINNEG2, H_LINNEG3 = 1 << 30, 1 << 31
 
 
 def phase_bits(w):
@@ -618,7 +626,8 @@ def phase_bits(w):
     if opc == OPC["lin"]:
         if ca == 1 and all(-1 <= c <= 1 for c in (cb, cc, cd)) and not (w[3] & FORCE_ACC) and \
                 (not ALL_ACC or PHASE_UNIT):
-            return H_LIN | (H_LINNEG if min(cb, cc, cd) < 0 else 0)
+            return (H_LIN | (H_LINNEG if min(cb, cc, cd) < 0 else 0) | (H_LINNEG2 if cc < 0 else 0) |
+                    (H_LINNEG3 if cb < 0 else 0))
         return H_ACC
     return H_RARE
 

@@ -27,6 +27,7 @@ from collections import Counter
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 H_MUL, H_MULNEG, H_FLAG, H_LIN, H_LINNEG, H_ACC, H_RARE, H_SELB = (1 << k for k in range(22, 30))
+H_LINNEG2, H_LINNEG3 = 1 << 30, 1 << 31
 H_ANY = H_MUL | H_LIN | H_ACC | H_RARE
 OPC = {"nop": 0, "muls": 1, "sgn0": 2, "lex": 3, "inv": 4, "lin": 5, "sel": 6, "eq": 7, "and": 8, "or": 9,
        "xor": 10, "st": 11, "selb": 12}
@@ -70,6 +71,8 @@ PATHS = {
     # r06 interpreter (fpvm.hpp): one / two-deep prefetch rings, bfe / bfi operand addresses,
     # negations on y only, per-block field decoding
     "r06": {
+        "lin_sum with negations, D only (r06x)": (94, "lin"),
+        "lin_sum with negations, C and D (r06x)": (94, "lin"),
         "loop: prefetch ring rotation + loop test": (4, "ring"),
         "loop: instruction / side-word prefetch": (4, "fetch"),
         "fill load issue (next phase fills)": (4, "spill"),
@@ -97,6 +100,10 @@ PATHS = {
         "fill write (scratch -> slot)": (2, "spill"),
     },
 }
+# r06x: lin_sum XORs only the positions some lane negates (H_LINNEG2 / H_LINNEG3; 12 VALU each)
+PATHS["r06x"] = dict(PATHS["r06"])
+PATHS["r06x"]["lin_sum with negations, D only (r06x)"] = (70, "lin")
+PATHS["r06x"]["lin_sum with negations, C and D (r06x)"] = (82, "lin")
 
 
 def load_prog(inc, name="VOTE"):
@@ -144,7 +151,14 @@ def phase_counts(w, nph, code, side):
                     c["lex compare (a lane with lex)"] += 1
         c["lin dispatch (unit / general)"] += 1
         if hdr & H_LIN:
-            c["lin_sum with negations (H_LINNEG)" if hdr & H_LINNEG else "lin_sum, unit signs"] += 1
+            if not hdr & H_LINNEG:
+                c["lin_sum, unit signs"] += 1
+            elif hdr & H_LINNEG3:
+                c["lin_sum with negations (H_LINNEG)"] += 1
+            elif hdr & H_LINNEG2:
+                c["lin_sum with negations, C and D (r06x)"] += 1
+            else:
+                c["lin_sum with negations, D only (r06x)"] += 1
             c["scale_reduce + store"] += 1
         if hdr & H_ACC:
             c["lin_mad (general coefficients, H_ACC)"] += 1
