@@ -325,3 +325,28 @@ def test_spill_pass_bounds_slots_and_keeps_values(hx, built, golden_votes):  # n
         sim = sched.simulate(sc, words, inp, r)
         assert sim == ref
         assert_same(run_vm(hx, consts, sc, words, inp, r, 0), sim, "vote %d spilled to %d" % (k, K))
+
+
+def test_batch_schedule_rules(built):
+    """The r06 scheduler rules on the batch vote programs (tools/fpvm/sched.py): every phase runs
+    one lin block (the unit block, or every lin op in the general one); a unit lin's negated
+    terms sit in its last positions (D, then C, then B), and the phase header's H_LINNEG2 /
+    H_LINNEG3 bits cover every lane that negates C / B (fpvm.hpp lin_sum XORs only those);
+    product phases are fuller than the r05 schedule's (lane use 0.833 on vote)."""
+    _, progs_ = built
+    for name in ("vote", "vote_t"):
+        _, sc, words, _, _ = progs_[name]
+        nw = sched.words_per_lane(sc.prog)
+        for t in range(sc.nrounds):
+            lanes = [words[(t * sc.W + l) * nw:(t * sc.W + l) * nw + 4] for l in range(sc.W)]
+            hdr = lanes[0][0] & ~0x3FFFFF
+            assert all(w[0] & ~0x3FFFFF == hdr for w in lanes), (name, t, "header differs between lanes")
+            for w in lanes:
+                b = sched.phase_bits(w)
+                assert b & hdr == b, (name, t, "lane needs a block the header lacks")
+                if (w[0] & 31) == sched.OPC["lin"] and b & sched.H_LIN and not b & sched.H_SELB:
+                    neg = [sched._s5((w[3] >> (5 * q)) & 31) < 0 for q in range(1, 4)]   # B, C, D
+                    n = sum(neg)
+                    assert neg == [False] * (3 - n) + [True] * n, (name, t, "negated terms not last", neg)
+        st = sc.stats()
+        assert st["lane_util_heavy"] > (0.87 if name == "vote" else 0.79), (name, st)
