@@ -36,6 +36,10 @@ PRODUCTS = ("muls", "sgn0", "lex", "eq")
 BANK_LANES, BANK_MOD = (int(x) for x in os.environ.get("OVH_BANK", "16,16").split(","))
 # passes of the bank-conflict local search over the slot assignment (improve_banks; 0 = off)
 BANK_PASSES = int(os.environ.get("OVH_BANK_PASSES", "3"))
+# result-store banking (ds_write_b128: 8-lane groups, residue mod 8) in the slot choice and the
+# local search; OVH_WBANK=0 models the reads alone (the r05 model)
+WBANK = os.environ.get("OVH_WBANK", "1") == "1"
+WBANK_LANES, WBANK_MOD = 8, 8
 # every lin op in the general-coefficient form (fpvm.hpp lin_mad): one linear block per phase
 # instead of the unit-sign block plus the general one; measured faster even for unit sums with
 # negations (r02aj: 1,013k -> 1,031-1,038k verifs/s). OVH_GEN_UNITLIN=1 with an interpreter
@@ -302,13 +306,18 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
                     seen_c.add((t, g, pos, c))
                     use[(t, g, pos)][c % BANK_MOD] += 1
 
+    # result stores: ds_write_b128 serves 8 contiguous lanes per pass over 32 banks, so the
+    # destination slots of lanes 8g .. 8g + 7 of a phase want distinct residues mod 8 (r06: the
+    # reads alone were modelled, and PMC put 36.5% of the LDS cycles in bank conflicts)
+    wuse = defaultdict(lambda: [0] * WBANK_MOD)
+
     def alloc(v):
         nonlocal nslots
         ev = [use[e] for e in reads[v]]
-        if v in lane_of:
-            ev.append(use[(def_round[v], lane_of[v] // BANK_LANES, "w")])
+        wv = wuse[(def_round[v], lane_of[v] // WBANK_LANES)] if (v in lane_of and WBANK) else None
         if free:
-            best = min(free, key=lambda x: (sum(u[x % BANK_MOD] for u in ev), x))
+            best = min(free, key=lambda x: (sum(u[x % BANK_MOD] for u in ev) +
+                                            (wv[x % WBANK_MOD] if wv is not None else 0), x))
             free.remove(best)
             s = best
         else:
@@ -316,6 +325,8 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
             nslots += 1
         for u in ev:
             u[s % BANK_MOD] += 1
+        if wv is not None:
+            wv[s % WBANK_MOD] += 1
         slot_of[v] = s
         lu = last_use[v]
         if lu < 0:   # never read (dead write): free right after
@@ -333,7 +344,8 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
     if max_slots is not None and nslots > max_slots:
         raise RuntimeError("%s: %d slots > %d" % (prog.name, nslots, max_slots))
     if BANK_PASSES and W == BANK_LANES:
-        improve_banks(prog, rounds, slot_of, def_round, last_use, nslots, consts, BANK_PASSES)
+        improve_banks(prog, rounds, slot_of, def_round, last_use, nslots, consts, BANK_PASSES,
+                      lane_of if WBANK else None)
     for i in pre:
         if ops[i].kind == "const":
             consts.ref(ops[i].imm, ops[i].name == "raw")
@@ -343,7 +355,7 @@ def schedule(prog, W, consts: ConstTable, max_slots=None, heavy_w=10, light_w=1,
     return sc
 
 
-def improve_banks(prog, rounds, slot_of, def_round, last_use, nslots, consts, passes):
+def improve_banks(prog, rounds, slot_of, def_round, last_use, nslots, consts, passes, lane_of=None):
     """Local search over the slot assignment against the ds_read_b128 bank model (the whole
     W-lane phase is one lane group; slot s and constant c hit bank group s, c mod BANK_MOD):
     a read costs max over residues of the distinct addresses with that residue, minus one, in
@@ -370,6 +382,13 @@ def improve_banks(prog, rounds, slot_of, def_round, last_use, nslots, consts, pa
                     key = ("c", c)
                 if key not in ctx[(t, pos)]:
                     ctx[(t, pos)].append(key)
+    # result stores (lane_of given): the destination slots of each 8-lane store group
+    if lane_of is not None:
+        for v, k in lane_of.items():
+            if v in slot_of and ops[v].kind not in ("st", "spill"):
+                c = (def_round[v], "w", k // WBANK_LANES)
+                ctx[c].append(("v", v))
+                reads_of[v].add(c)
 
     def res(key, moved=None, r=None):
         if key[0] == "c":
@@ -379,6 +398,11 @@ def improve_banks(prog, rounds, slot_of, def_round, last_use, nslots, consts, pa
         return slot_of[key[1]] % BANK_MOD
 
     def cost(c, moved=None, r=None):
+        if c[1] == "w":   # a store group: residues mod WBANK_MOD (r: a residue mod BANK_MOD)
+            cnt = [0] * WBANK_MOD
+            for key in ctx[c]:
+                cnt[res(key, moved, r) % WBANK_MOD] += 1
+            return max(cnt) - 1
         cnt = [0] * BANK_MOD
         for key in ctx[c]:
             cnt[res(key, moved, r)] += 1
