@@ -14,8 +14,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def hx():
     out = os.path.join(ROOT, "tests", "host", "_build", "libhx.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", out,
+    # built under a per-process name and renamed into place: parallel workers (pytest -n) never
+    # load a half-written library
+    tmp = "%s.%d" % (out, os.getpid())
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", tmp,
                            os.path.join(ROOT, "tests", "host", "harness.cpp")])
+    os.replace(tmp, out)
     return ctypes.CDLL(out)
 
 
